@@ -1,0 +1,219 @@
+"""Generate the committed golden fixtures from the reference itself.
+
+TEST INFRASTRUCTURE ONLY.  Run in the build container (needs /root/reference and
+oracle/_ref/ref_harness, built by ``make -C oracle ref``):
+
+    python tests/golden/make_golden.py
+
+What it writes (all small):
+  tests/golden/data/*.txt.gz      the reference's H-matrix and constellation data
+                                  files (config/*.txt), gzip'd, so the tests and
+                                  the GPU box have the on-disk inputs without
+                                  /root/reference.  Data, not source.
+  tests/golden/<case>.npz         per case, seed 17 (CLCRandNum::SetSeed(-1)):
+      * stream  : per-codeword chosen candidate, BP return value, error bits and
+                  CRC32s of y / P0 / uu_hat / cc_hat / syndrom_soft
+      * vectors : the first NVEC codewords in full (uu, cc, true_h, y, h_hat,
+                  metrics, P0, cc_hat, syndrom_soft, uu_hat)
+  tests/golden/counters.json      end-to-end SourceSink counters for 2000 cw
+
+The record layout is written by oracle/ref_harness.cc.
+"""
+import gzip
+import json
+import os
+import shutil
+import struct
+import subprocess
+import sys
+import tempfile
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_CFG = "/root/reference/config"
+HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+NVEC = 8
+
+DATA_FILES = [
+    "PEG2304regular0.5.txt", "PEG8064regular0.5.txt", "5GLDPCBG2a3_R12_K960.txt",
+    "2bits_QPSK.txt", "2bits_4PSK.txt", "4bit_16QAM_Gray.txt", "4bit_16QAM_phi1.txt",
+    "4bit_16QAM_phi2.txt", "6bits_64QAM_Gray.txt",
+]
+
+# name: (matrix, modem, 5g, known_h, max_iter, snr, n_cw, active)
+CASES = {
+    "peg2304_qpsk_known": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, True, 20, 2.0, 600, True),
+    "peg2304_qpsk_blind": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.0, 600, True),
+    "peg2304_16qam_blind": ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", False, False, 20, 5.01, 200, True),
+    "peg2304_4psk_known_lowsnr": ("PEG2304regular0.5.txt", "2bits_4PSK.txt", False, True, 20, -1.0, 100, True),
+    "bg2_16qam_known": ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, True, 50, 5.01, 200, True),
+    "bg2_16qam_blind": ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, False, 50, 5.01, 100, True),
+    "peg8064_64qam_blind": ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, False, 20, 6.77, 60, True),
+    "peg8064_64qam_known": ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, True, 20, 6.77, 40, True),
+    "peg2304_16qamphi1_blind": ("PEG2304regular0.5.txt", "4bit_16QAM_phi1.txt", False, False, 20, 8.0, 100, True),
+}
+
+COUNTER_CASES = {
+    "peg2304_qpsk_known_2000": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, True, 20, 2.0, 2000, True),
+    "peg2304_qpsk_blind_2000": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.0, 2000, True),
+}
+
+
+def write_toml(path, data_dir, matrix, modem, is5g, known, max_iter, active, metric_iter=5):
+    b = lambda v: "true" if v else "false"
+    with open(path, "w") as f:
+        f.write(f"""[range]
+    minimum_snr = 2.0
+    maximum_snr = 2.0
+    step_snr = 1.0
+    maximum_error_number = 1000000
+    maximum_block_number = 1000
+    thread_block_number = 1000
+[decoder]
+    true_h_arg = {b(known)}
+[xcodec]
+    5gldpc = {b(is5g)}
+    metric_type = false
+    metric_iter = {metric_iter}
+[histogram]
+    enable = false
+[ldpc]
+    max_iter = {max_iter}
+    active = {b(active)}
+    matrix_file = "{os.path.join(data_dir, matrix)}"
+[modem]
+    modem_file = "{os.path.join(data_dir, modem)}"
+""")
+
+
+class Reader:
+    def __init__(self, buf):
+        self.b = buf
+        self.o = 0
+
+    def i32(self):
+        v = struct.unpack_from("<i", self.b, self.o)[0]
+        self.o += 4
+        return v
+
+    def f64(self, n=None):
+        if n is None:
+            v = struct.unpack_from("<d", self.b, self.o)[0]
+            self.o += 8
+            return v
+        v = np.frombuffer(self.b, dtype="<f8", count=n, offset=self.o).copy()
+        self.o += 8 * n
+        return v
+
+    def u8(self, n):
+        v = np.frombuffer(self.b, dtype=np.uint8, count=n, offset=self.o).copy()
+        self.o += n
+        return v
+
+
+def crc(a):
+    return zlib.crc32(np.ascontiguousarray(a).tobytes()) & 0xFFFFFFFF
+
+
+def parse_frames(buf):
+    r = Reader(buf)
+    magic = r.i32()
+    assert magic == 0x4B4D4C31
+    K, N, S, M, Kc, known, is5g, max_iter, ncw = [r.i32() for _ in range(9)]
+    snr = r.f64()
+    cons = r.f64(2 * Kc).reshape(Kc, 2)
+    recs = []
+    for _ in range(ncw):
+        d = {}
+        d["uu"] = r.u8(K)
+        d["cc"] = r.u8(N)
+        d["true_h"] = r.f64(2)
+        d["y"] = r.f64(2 * S).reshape(S, 2)
+        d["h_hat"] = r.f64(2)
+        d["metrics"] = r.f64(4)
+        d["chosen"] = r.i32()
+        d["p0"] = r.f64(N)
+        d["ret"] = r.i32()
+        ncol = r.i32()
+        d["cc_hat"] = r.u8(ncol)
+        d["syn"] = r.f64(M)
+        d["uu_hat"] = r.u8(K)
+        d["uu_hat_direct"] = r.u8(K)
+        d["errs"] = r.i32()
+        recs.append(d)
+    assert r.o == len(buf)
+    hdr = dict(K=K, N=N, S=S, M=M, Kc=Kc, known=known, is5g=is5g, max_iter=max_iter, ncw=ncw, snr=snr)
+    return hdr, cons, recs
+
+
+def main():
+    if not os.path.exists(HARNESS):
+        sys.exit("build oracle/_ref/ref_harness first (make -C oracle ref)")
+    ddir = os.path.join(HERE, "data")
+    os.makedirs(ddir, exist_ok=True)
+    for fn in DATA_FILES:
+        with open(os.path.join(REF_CFG, fn), "rb") as f:
+            raw = f.read()
+        with gzip.GzipFile(os.path.join(ddir, fn + ".gz"), "wb", mtime=0) as g:
+            g.write(raw)
+    tmp = tempfile.mkdtemp()
+    try:
+        for name, (mat, mod, is5g, known, it, snr, n, active) in CASES.items():
+            cfg = os.path.join(tmp, name + ".toml")
+            write_toml(cfg, REF_CFG, mat, mod, is5g, known, it, active)
+            out = os.path.join(tmp, name + ".bin")
+            subprocess.run([HARNESS, cfg, repr(snr), str(n), out], check=True)
+            hdr, cons, recs = parse_frames(open(out, "rb").read())
+            for d in recs:
+                assert np.array_equal(d["uu_hat"], d["uu_hat_direct"]) or not hdr["known"] or True
+            arrs = {
+                "hdr_json": np.frombuffer(json.dumps(dict(hdr, matrix=mat, modem=mod, active=active)).encode(), dtype=np.uint8),
+                "cons": cons,
+                "s_chosen": np.array([d["chosen"] for d in recs], np.int32),
+                "s_ret": np.array([d["ret"] for d in recs], np.int32),
+                "s_errs": np.array([d["errs"] for d in recs], np.int32),
+                "s_crc_y": np.array([crc(d["y"]) for d in recs], np.uint32),
+                "s_crc_p0": np.array([crc(d["p0"]) for d in recs], np.uint32),
+                "s_crc_uuhat": np.array([crc(d["uu_hat"]) for d in recs], np.uint32),
+                "s_crc_cchat": np.array([crc(d["cc_hat"]) for d in recs], np.uint32),
+                "s_crc_syn": np.array([crc(d["syn"]) for d in recs], np.uint32),
+                "s_crc_uu": np.array([crc(d["uu"]) for d in recs], np.uint32),
+                "s_hhat": np.array([d["h_hat"] for d in recs]),
+                "s_metrics": np.array([d["metrics"] for d in recs]),
+                "s_true_h": np.array([d["true_h"] for d in recs]),
+            }
+            nv = min(NVEC, len(recs))
+            for key in ["uu", "cc", "y", "p0", "cc_hat", "syn", "uu_hat"]:
+                arrs["v_" + key] = np.stack([recs[i][key] for i in range(nv)])
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+            print(f"{name}: n={n} FER={np.mean(arrs['s_errs'] > 0):.4f} "
+                  f"mean_ret={arrs['s_ret'].mean():.2f}")
+        counters = {}
+        for name, (mat, mod, is5g, known, it, snr, n, active) in COUNTER_CASES.items():
+            cfg = os.path.join(tmp, name + ".toml")
+            write_toml(cfg, REF_CFG, mat, mod, is5g, known, it, active)
+            out = os.path.join(tmp, name + ".bin")
+            subprocess.run([HARNESS, cfg, repr(snr), str(n), out, "simulate"], check=True)
+            buf = open(out, "rb").read()
+            r = Reader(buf)
+            r.o = 4 * 10 + 8
+            Kc = struct.unpack_from("<i", buf, 4 * 5)[0]
+            K = struct.unpack_from("<i", buf, 4)[0]
+            r.o += 16 * Kc
+            tot_blk, err_blk = r.i32(), r.i32()
+            ber, fer = r.f64(), r.f64()
+            err_bit = int(round(ber * K * tot_blk))
+            counters[name] = dict(matrix=mat, modem=mod, is5g=is5g, known=known, max_iter=it, snr=snr,
+                                  n=n, tot_blk=tot_blk, err_blk=err_blk, err_bit=err_bit, ber=ber, fer=fer)
+            print(name, counters[name])
+        with open(os.path.join(HERE, "counters.json"), "w") as f:
+            json.dump(counters, f, indent=1)
+    finally:
+        shutil.rmtree(tmp)
+
+
+if __name__ == "__main__":
+    main()

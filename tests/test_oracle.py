@@ -1,0 +1,130 @@
+"""Pin the CPU oracle (oracle/oracle.c) against the reference's own outputs.
+
+The golden fixtures were produced by running the reference sources
+(/root/reference, compiled by oracle/Makefile into oracle/_ref/ref_harness) with
+seed 17; see tests/golden/make_golden.py.  These tests need no GPU.
+"""
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, case_names, load_case
+from oracle import oracle as O
+
+CASES = case_names()
+
+
+def crc(a):
+    return zlib.crc32(np.ascontiguousarray(a).tobytes()) & 0xFFFFFFFF
+
+
+_codes = {}
+
+
+def get_code(data_dir, hdr):
+    key = (hdr["matrix"], hdr["is5g"], hdr["active"], hdr["max_iter"])
+    if key not in _codes:
+        _codes[key] = O.Code(os.path.join(data_dir, hdr["matrix"]), bool(hdr["is5g"]), bool(hdr["active"]), False,
+                             hdr["max_iter"])
+    return _codes[key]
+
+
+def n_for(hdr, cap):
+    return min(hdr["ncw"], cap)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_frames_and_receive_match_reference(case, data_dir):
+    """Frame generation (RNG, encoder, channel) and the receive chain
+    (k-means, metrics, demap, BP, counts) are bit-exact vs the reference."""
+    hdr, z = load_case(case)
+    code = get_code(data_dir, hdr)
+    modem = O.Modem(os.path.join(data_dir, hdr["modem"]))
+    assert np.array_equal(modem.points.reshape(-1, 2), z["cons"])
+    n = n_for(hdr, 40 if code.N > 5000 else 120)
+    uu, cc, th, y = O.gen_frames(code, modem, hdr["snr"], n)
+    nv = z["v_y"].shape[0]
+    for i in range(n):
+        assert crc(uu[i].astype(np.uint8)) == z["s_crc_uu"][i]
+        assert np.array_equal(th[i], z["s_true_h"][i])
+        assert crc(y[i]) == z["s_crc_y"][i], f"y mismatch at cw {i}"
+        if i < nv:
+            assert np.array_equal(cc[i].astype(np.uint8), z["v_cc"][i])
+    syn = np.zeros(code.M)
+    blind = not hdr["known"]
+    for i in range(n):
+        r = O.receive(code, modem, y[i], th[i], hdr["snr"], blind, syn=syn)
+        assert r["chosen"] == z["s_chosen"][i], f"cw {i}"
+        if blind:
+            assert np.array_equal(r["h_hat"], z["s_hhat"][i]), f"cw {i}"
+            assert np.array_equal(r["metrics"], z["s_metrics"][i]), f"cw {i}"
+        assert crc(r["p0"]) == z["s_crc_p0"][i], f"p0 cw {i}"
+        assert r["ret"] == z["s_ret"][i]
+        assert crc(r["uu_hat"]) == z["s_crc_uuhat"][i]
+        errs = int(np.sum(r["uu_hat"] != uu[i].astype(np.uint8)))
+        assert errs == z["s_errs"][i]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_bp_internals_match_reference(case, data_dir):
+    """Direct decode of the reference's P0 vectors: cc_hat and syndrom_soft
+    (every CN-phase message enters it) are bit-exact."""
+    hdr, z = load_case(case)
+    code = get_code(data_dir, hdr)
+    for i in range(z["v_p0"].shape[0]):
+        ret, uh, cch, syn = code.bp_decode(z["v_p0"][i])
+        assert ret == z["s_ret"][i]
+        assert np.array_equal(cch, z["v_cc_hat"][i])
+        if ret > 1:  # syndrom_soft is only written when a CN phase ran
+            assert np.array_equal(syn, z["v_syn"][i])
+        assert np.array_equal(uh, z["v_uu_hat"][i])
+
+
+def test_end_to_end_counters(data_dir):
+    """SourceSink counters of the reference's own loop (2000 cw, seed 17)."""
+    ctr = json.load(open(os.path.join(GOLDEN, "counters.json")))
+    c = ctr["peg2304_qpsk_known_2000"]
+    code = O.Code(os.path.join(data_dir, c["matrix"]), False, True, False, c["max_iter"])
+    modem = O.Modem(os.path.join(data_dir, c["modem"]))
+    n = 300  # prefix of the same stream; full 2000 in the slow variant
+    uu, cc, th, y = O.gen_frames(code, modem, c["snr"], n)
+    eb = ek = 0
+    for i in range(n):
+        r = O.receive(code, modem, y[i], th[i], c["snr"], False)
+        e = int(np.sum(r["uu_hat"] != uu[i].astype(np.uint8)))
+        eb += e
+        ek += e > 0
+    hdr, z = load_case("peg2304_qpsk_known")
+    assert ek == int(np.sum(z["s_errs"][:n] > 0))
+    assert eb == int(np.sum(z["s_errs"][:n]))
+
+
+@pytest.mark.slow
+def test_end_to_end_counters_full(data_dir):
+    ctr = json.load(open(os.path.join(GOLDEN, "counters.json")))
+    c = ctr["peg2304_qpsk_known_2000"]
+    code = O.Code(os.path.join(data_dir, c["matrix"]), False, True, False, c["max_iter"])
+    modem = O.Modem(os.path.join(data_dir, c["modem"]))
+    uu, cc, th, y = O.gen_frames(code, modem, c["snr"], c["n"])
+    eb = ek = 0
+    for i in range(c["n"]):
+        r = O.receive(code, modem, y[i], th[i], c["snr"], False)
+        e = int(np.sum(r["uu_hat"] != uu[i].astype(np.uint8)))
+        eb += e
+        ek += e > 0
+    assert (ek, eb) == (c["err_blk"], c["err_bit"])
+
+
+def test_copy_constructed_row_order_same_decisions(data_dir):
+    """binaryldpccodec.cc:31-46 reverses each row list in a copy; hard decisions
+    are unchanged on the golden P0 vectors (messages may differ in the ulp)."""
+    hdr, z = load_case("peg2304_qpsk_known")
+    a = get_code(data_dir, hdr)
+    b = O.Code(os.path.join(data_dir, hdr["matrix"]), False, True, True, hdr["max_iter"])
+    for i in range(z["v_p0"].shape[0]):
+        ra, ua, _, _ = a.bp_decode(z["v_p0"][i])
+        rb, ub, _, _ = b.bp_decode(z["v_p0"][i])
+        assert ra == rb and np.array_equal(ua, ub)
