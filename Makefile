@@ -1,0 +1,39 @@
+# Top-level build: the product library (gfx950 HIP) and the test oracle.
+#
+#   make            -> kmldpc_amd/libkmldpc_amd.so, kmldpc_amd/bin/kmldpc_gpu, oracle/*
+#   make lib        -> product library only
+#   make oracle     -> oracle/liboracle.so, oracle/cpu_baseline (+ oracle/_ref when /root/reference exists)
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result -Wno-unused-value
+CSRC     := kmldpc_amd/csrc
+OBJDIR   := build/obj
+CPP_SRCS := config code modem capi
+HIP_SRCS := bp demap kmeans framegen
+OBJS     := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(CPP_SRCS) $(HIP_SRCS)))
+HDRS     := $(wildcard $(CSRC)/*.hpp) include/kmldpc_amd.h
+LIB      := kmldpc_amd/libkmldpc_amd.so
+
+all: lib oracle
+
+lib: $(LIB)
+
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,-rpath,/opt/rocm/lib
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all lib oracle clean

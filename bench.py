@@ -1,0 +1,248 @@
+"""Throughput benchmark of the kmldpc receive path on MI355X.
+
+Workload (BASELINE.json configs[1]): PEG2304 R=1/2 + QPSK, Es/N0 = 2.0 dB
+(= Eb/N0 2 dB), max 20 BP iterations, known-channel ("ideal") demap, a batch of
+B synthetic y = h*x + w frames per GPU generated on the GPU before the timed
+region (resident in HBM).  One step = demap + sum-product BP (+ error
+counting) over the whole resident batch, i.e. KmCodec::Decoder + SourceSink::CntErr
+(src/kmcodec.cc:54-72, lib/lab/src/sourcesink.cc:29-47) for B codewords.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--blind]
+
+N > 1 is launched by torch.distributed.run, one process per GPU; frames are
+sharded by global codeword index (weak scaling, no data-path collective) and
+the error counters are summed with one RCCL all-reduce at the end.
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import gzip
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import kmldpc_amd as K  # noqa: E402  (load the HIP library before torch)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+
+
+def data_dir():
+    d = tempfile.mkdtemp(prefix="kml_bench_")
+    src = os.path.join(REPO, "tests", "golden", "data")
+    for fn in os.listdir(src):
+        if fn.endswith(".gz"):
+            with gzip.open(os.path.join(src, fn), "rb") as g, open(os.path.join(d, fn[:-3]), "wb") as f:
+                f.write(g.read())
+    return d
+
+
+def write_config(d, args):
+    cfg = os.path.join(d, "config.toml")
+    with open(cfg, "w") as f:
+        f.write(f"""[range]
+    minimum_snr = {args.snr!r}
+    maximum_snr = {args.snr!r}
+    step_snr = 1.0
+    maximum_error_number = 1000000000
+    maximum_block_number = 1000000000
+    thread_block_number = {args.batch}
+[decoder]
+    true_h_arg = {"false" if args.blind else "true"}
+[xcodec]
+    5gldpc = {"true" if args.is5g else "false"}
+    metric_type = false
+    metric_iter = 5
+[histogram]
+    enable = false
+[ldpc]
+    max_iter = {args.max_iter}
+    active = true
+    matrix_file = "{args.matrix}"
+[modem]
+    modem_file = "{args.modem}"
+""")
+    return cfg
+
+
+def cpu_baseline(d, args):
+    """The oracle restatement of the same receive path timed on host cores
+    (reported baseline; test infrastructure, never the measured product)."""
+    exe = os.path.join(REPO, "oracle", "cpu_baseline")
+    if not os.path.exists(exe):
+        return None
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))
+    n = args.cpu_cw_per_thread
+    cmd = [exe, os.path.join(d, args.matrix), os.path.join(d, args.modem), str(int(args.is5g)), repr(args.snr),
+           str(args.max_iter), str(int(args.blind)), str(n), str(threads)]
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+    except Exception as e:  # pragma: no cover
+        print(f"cpu_baseline failed: {e}", file=sys.stderr)
+        return None
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(r["cw_per_s"], 3), "unit": "codewords/s", "cores": threads, "kind": "port",
+            "sample": f"{r['codewords']} codewords ({n}/thread x {threads} threads) of the same workload through "
+                      f"oracle/ (C restatement of KmCodec::Decoder + CntErr, bit-exact vs reference), "
+                      f"{r['seconds']:.1f} s; FER {r['fer']:.4f}",
+            "cpu_model": cpu_model}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=32768, help="codewords per GPU per step")
+    ap.add_argument("--snr", type=float, default=2.0, help="Es/N0 in dB (reference 'snr')")
+    ap.add_argument("--max-iter", type=int, default=20)
+    ap.add_argument("--matrix", default="PEG2304regular0.5.txt")
+    ap.add_argument("--modem", default="2bits_QPSK.txt")
+    ap.add_argument("--is5g", action="store_true")
+    ap.add_argument("--blind", action="store_true")
+    ap.add_argument("--seed", type=int, default=17)
+    ap.add_argument("--cpu-cw-per-thread", type=int, default=5000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+
+        torch.cuda.set_device(local)
+        dist_mod.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        dist = dist_mod
+
+    d = data_dir()
+    cfg = write_config(d, args)
+    ctx = K.Context(cfg, data_dir=d, device=local)
+    B = args.batch
+    # frames for global codeword indices [rank*B, (rank+1)*B): resident in HBM
+    ctx.sim_generate(args.snr, B, seed=args.seed, first_cw=rank * B)
+
+    def barrier():
+        ctx.sync()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        ctx.sim_decode(args.snr, blind=args.blind, sync=False)
+    barrier()
+    ctx.prof_reset()
+    ctx.prof_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.sim_decode(args.snr, blind=args.blind, sync=False)
+    barrier()
+    t1 = time.perf_counter()
+    ctx.prof_enable(False)
+    elapsed = t1 - t0
+    bp = ctx.prof_read("bp")
+    stages = {s: ctx.prof_read(s) for s in ("demap", "kmeans", "metric")}
+    # one more (untimed) pass for the statistical counters
+    c = ctx.sim_decode(args.snr, blind=args.blind)
+
+    import numpy as np
+    vals = np.array([c["err_bit"], c["err_blk"], c["tot_bit"], c["tot_blk"], c["vn_phases"], c["cn_phases"]],
+                    dtype=np.float64)
+    t_max = elapsed
+    if dist is not None:
+        import torch
+        tv = torch.tensor(vals, device="cuda")
+        dist.all_reduce(tv)  # RCCL over xGMI: the only collective
+        vals = tv.cpu().numpy()
+        tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    total_cw = B * args.steps * world
+    value = total_cw / t_max
+    err_bit, err_blk, tot_bit, tot_blk, vn, cn = vals
+    bp_avg_ms = bp["ms"] / max(bp["launches"], 1)
+    bp_bytes = bp["bytes"] / max(bp["launches"], 1)
+    achieved = bp_bytes / (bp_avg_ms * 1e-3) / 1e9 if bp_avg_ms > 0 else 0.0
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_bp.json")
+    if os.path.exists(pmc):
+        try:
+            pm = json.load(open(pmc))
+            if pm.get("batch") == B and pm.get("workload") == args.matrix:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    line = {
+        "metric": "decoded codewords/sec (N=2304 R=1/2, 20 BP iters) at 1/2/4/8 GPUs; BER match",
+        "value": round(value, 1),
+        "unit": "codewords/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(t_max / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic y=h*x+w frames generated on the GPU (Philox), resident in HBM before timing",
+        "config": {
+            "workload": f"{args.matrix.split('.txt')[0]} + {args.modem.split('.txt')[0]}, Es/N0 {args.snr} dB, "
+                        f"max {args.max_iter} BP iters, {'blind k-means' if args.blind else 'known-H ideal'} demap",
+            "batch_per_gpu": B,
+            "global_batch": B * world,
+            "parallelism": f"codeword-sharded x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "bp_kernel (sum-product BP, messages LDS-resident)",
+            "alg_bytes_per_launch": round(bp_bytes),
+            "avg_launch_ms": round(bp_avg_ms, 4),
+            "alg_bytes_rule": "SURVEY 8(d): VN phase 24E+9N B, CN phase 24E B, + 8*cc_len B P0 per codeword",
+        },
+        "stats": {
+            "fer": err_blk / max(tot_blk, 1),
+            "ber": err_bit / max(tot_bit, 1),
+            "mean_cn_phases": cn / max(tot_blk, 1),
+            "mean_vn_phases": vn / max(tot_blk, 1),
+            "stage_ms_per_step": {s: round(v["ms"] / max(args.steps, 1), 4) for s, v in stages.items() if v["launches"]},
+            "bp_ms_per_step": round(bp["ms"] / max(args.steps, 1), 4),
+        },
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(d, args)
+    print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

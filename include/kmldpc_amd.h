@@ -1,0 +1,157 @@
+/* kmldpc_amd.h — C ABI of the MI355X-native kmldpc hot path.
+ *
+ * Drop-in boundary for the per-codeword receive loop of trganda/kmldpc
+ * (paths relative to /root/reference/kmldpc).  The reference has no FFI; its
+ * boundary is a set of C++ classes.  Each entry point below replaces one of
+ * them, batched over B codewords:
+ *
+ *   kml_create                lab::BinaryLDPCCodec(const toml::value&)            lib/lab/include/binaryldpccodec.h:16
+ *                             lab::Binary5GLDPCCodec(const toml::value&)           lib/lab/include/binary5gldpccodec.h:12
+ *                             lab::Modem(const toml::value&)                       lib/lab/include/modem.h:13
+ *                             KmCodec(toml::value)                                 include/kmcodec.h:16
+ *   kml_bp_decode             virtual int BinaryLDPCCodec::Decoder(const double *M2V, int *uu_hat, int iter_count)
+ *                                                                                  lib/lab/include/binaryldpccodec.h:20
+ *                                                                                  (override binary5gldpccodec.h:17)
+ *   kml_demap                 void ModemLinearSystem::DeMapping(thetaList, double *bitLin, double *bitLout)
+ *                                                                                  lib/lab/include/modemlinearsystem.h:20-22
+ *   kml_kmeans                kmldpc::KMeans(data, constellations, iter); Run(); clusters()
+ *                                                                                  include/kmeans.h:14-22
+ *                             + h_hat = clusters[0]/c[0] and its 4 rotations       src/simulator.cc:145-148
+ *   kml_decode_frames         void KmCodec::Decoder(ModemLinearSystem&, const std::vector<complex>& h_hats, int *uu_hat)
+ *                                                                                  include/kmcodec.h:23-25
+ *   kml_count_errors          void SourceSink::CntErr(const int*, const int*, int, int)  lib/lab/include/sourcesink.h:15
+ *   kml_sim_*                 the throughput driver: frame generation + receive + counting for one
+ *                             SNR point of Simulator::run_blocks (src/simulator.cc:112-168)
+ *
+ * Conventions
+ *   - Every call returns 0 on success or a negative KML_E* code and never exits
+ *     the process (the reference logs and exit(-1)s).  kml_last_error() holds
+ *     the message of the last failure on that context.
+ *   - Bits (uu, uu_hat, cc_hat) are one byte per bit (0/1) unless a name says
+ *     "_bits" (packed little-endian uint64 words).  Complex numbers are
+ *     interleaved (re, im) doubles.
+ *   - Pointers are host pointers unless KML_DEVICE_PTRS is set in `flags`, in
+ *     which case they must be device pointers on the context's GPU; results are
+ *     complete when the call returns (the context's HIP stream is synchronised).
+ *   - A context is bound to one GPU and one HIP stream and is not thread-safe;
+ *     use one context per GPU / per thread.
+ */
+#ifndef KMLDPC_AMD_H
+#define KMLDPC_AMD_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KML_ABI_VERSION 1
+
+enum {
+  KML_OK = 0,
+  KML_E_ARG = -1,    /* bad argument */
+  KML_E_IO = -2,     /* cannot open / parse a config, H-matrix or constellation file */
+  KML_E_HIP = -3,    /* HIP runtime failure */
+  KML_E_UNSUP = -4,  /* configuration not supported */
+  KML_E_NOMEM = -5
+};
+
+enum { KML_DEVICE_PTRS = 1 };
+
+typedef struct kml_ctx kml_ctx;
+
+/* dims[]: index names for kml_dims */
+enum {
+  KML_DIM_M = 0,        /* check rows */
+  KML_DIM_NCOL = 1,     /* internal columns (incl. punctured) */
+  KML_DIM_K = 2,        /* info bits (code_dim) */
+  KML_DIM_CCLEN = 3,    /* transmitted bits */
+  KML_DIM_Z = 4,        /* 5G lifting factor */
+  KML_DIM_E = 5,        /* edges */
+  KML_DIM_CHK = 6,      /* GF(2) rank (code_chk) */
+  KML_DIM_MAXITER = 7,  /* [ldpc] max_iter */
+  KML_DIM_BITS = 8,     /* bits per symbol */
+  KML_DIM_KC = 9,       /* constellation points */
+  KML_DIM_S = 10,       /* symbols per codeword */
+  KML_DIM_BP_LDS = 11,  /* 1 if the decoder keeps messages in LDS */
+  KML_DIM_COUNT = 12
+};
+
+/* Create a context from a reference config.toml.  Relative matrix_file /
+ * modem_file paths are resolved against data_dir (NULL or "" = the CWD, as
+ * the reference does).  device = HIP device ordinal; device < 0 creates a
+ * host-only context (planner, encoder, constellation; no GPU calls). */
+int kml_create(const char *config_toml, const char *data_dir, int device, kml_ctx **out);
+/* Same without a config file: the [ldpc]/[modem]/[xcodec] keys given directly. */
+int kml_create_explicit(const char *matrix_file, const char *modem_file, int is5g, int active, int max_iter,
+                        int metric_soft, int metric_iter, int device, kml_ctx **out);
+void kml_destroy(kml_ctx *ctx);
+const char *kml_last_error(const kml_ctx *ctx);
+int kml_abi_version(void);
+
+int kml_dims(const kml_ctx *ctx, int32_t *dims /* [KML_DIM_COUNT] */);
+/* Host-side code plan, for inspection and parity tests. */
+int kml_code_perm(const kml_ctx *ctx, int32_t *perm /* [Ncol] */);
+int kml_code_graph(const kml_ctx *ctx, int32_t *row_ptr /* [M+1] */, int32_t *row_col /* [E] */,
+                   int32_t *col_ptr /* [Ncol+1] */, int32_t *col_slot /* [E] */);
+int kml_constellation(const kml_ctx *ctx, double *points /* [2*Kc] */);
+/* Host encoder (BinaryLDPCCodec::Encoder), uu[K] -> cc[cc_len], bytes. */
+int kml_encode(const kml_ctx *ctx, const uint8_t *uu, uint8_t *cc, int B);
+
+/* BinaryLDPCCodec::Decoder, batched.  p0[B][cc_len] = P(bit = 0) (the
+ * reference's M2V).  Outputs (any may be NULL): uu_hat[B][K], ret[B] (the
+ * reference return value iter + (iter < max_iter)), cc_hat[B][Ncol],
+ * syn[B][M] (syndrom_soft; rows are only written when a CN phase runs, like
+ * the reference's member array). */
+int kml_bp_decode(kml_ctx *ctx, const double *p0, int B, int iter_count, uint8_t *uu_hat, int32_t *ret,
+                  uint8_t *cc_hat, double *syn, int flags);
+
+/* ModemLinearSystem::DeMapping with bitLin = 0.5 and one channel estimate per
+ * codeword: y[B][S][2], h[B][2], var = 10^(-snr/10) -> p0[B][cc_len]. */
+int kml_demap(kml_ctx *ctx, const double *y, const double *h, double var, int B, double *p0, int flags);
+
+/* KMeans(y, constellation, iters).Run(); h_hat = clusters[0]/c[0];
+ * h4[j] = h_hat * exp(i*kPi/2*j).  h_hat[B][2], h4[B][4][2] (either may be NULL). */
+int kml_kmeans(kml_ctx *ctx, const double *y, int B, int iters, double *h_hat, double *h4, int flags);
+
+/* KmCodec::Decoder for B codewords at Es/N0 = snr dB.  true_h[B][2] selects
+ * the known-channel path ([decoder] true_h_arg = true); true_h == NULL runs the
+ * blind path (k-means, 4 candidates, syndrome metric).  Optional outputs:
+ * chosen[B], metrics[B][4], ret[B], h_hat[B][2]. */
+int kml_decode_frames(kml_ctx *ctx, const double *y, const double *true_h, double snr, int B, uint8_t *uu_hat,
+                      int32_t *chosen, double *metrics, int32_t *ret, double *h_hat, int flags);
+
+/* SourceSink::CntErr over B codewords; counters[4] += {err_bit, err_blk, tot_bit, tot_blk}. */
+int kml_count_errors(kml_ctx *ctx, const uint8_t *uu, const uint8_t *uu_hat, int B, uint64_t *counters, int flags);
+
+/* --- throughput driver (GPU-resident frames) ----------------------------- */
+/* Generate B frames for codeword indices [first_cw, first_cw + B) at Es/N0 =
+ * snr into the context's resident buffers (Philox stream keyed by seed). */
+int kml_sim_generate(kml_ctx *ctx, double snr, uint64_t seed, uint64_t first_cw, int B);
+/* Receive the resident batch (blind or known-H) and accumulate the counters.
+ * counters[8] (may be NULL) receives {err_bit, err_blk, tot_bit, tot_blk,
+ * vn_phases, cn_phases, converged, 0} of this call.  If sync == 0 the call
+ * returns after enqueueing the work (counters must then be NULL); use
+ * kml_sync to wait. */
+int kml_sim_decode(kml_ctx *ctx, double snr, int blind, uint64_t *counters, int sync);
+int kml_sync(kml_ctx *ctx);
+/* Copy the resident frames out (for checks): uu[B][K] bytes, y[B][S][2], h[B][2]. */
+int kml_sim_frames(kml_ctx *ctx, uint8_t *uu, double *y, double *h);
+
+/* --- profiling ----------------------------------------------------------- */
+/* When enabled, every kernel launch of the context is bracketed by HIP events
+ * on the context's stream.  kml_prof_read returns, for the named stage
+ * ("bp", "demap", "kmeans", "metric", "framegen"), the number of launches,
+ * their summed device time in ms and the summed algorithmic bytes
+ * (SURVEY §8d accounting for "bp"). */
+int kml_prof_enable(kml_ctx *ctx, int on);
+int kml_prof_reset(kml_ctx *ctx);
+int kml_prof_read(kml_ctx *ctx, const char *stage, int64_t *launches, double *total_ms, double *alg_bytes);
+
+/* Device-side probe of the exact-math helpers: in[n][4] = (a, b, c, d) ->
+ * out[n][4] = (hypot(a,b), re((a+ib)/(c+id)), im(...), exp(a)). */
+int kml_math_probe(kml_ctx *ctx, const double *in, int n, double *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

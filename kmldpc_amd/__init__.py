@@ -1,0 +1,339 @@
+"""kmldpc_amd — MI355X-native kmldpc receive path (BP decoder + k-means blind demap).
+
+Python face of the C ABI in include/kmldpc_amd.h (libkmldpc_amd.so, built for
+gfx950 by `make lib` / __graft_entry__.build()).  There is no CPU fallback: if
+the shared library is missing or the GPU is unavailable, every GPU entry point
+raises.  The class names mirror the reference's C++ interface
+(/root/reference/kmldpc):
+
+    Context                    config.toml + H-matrix + constellation (KmCodec / BinaryLDPCCodec / Modem ctors)
+    Context.bp_decode          lab::BinaryLDPCCodec::Decoder            lib/lab/src/binaryldpccodec.cc:165-278
+    Context.demap              lab::ModemLinearSystem::DeMapping         lib/lab/src/modemlinearsystem.cc:93-98
+    Context.kmeans             kmldpc::KMeans::Run + simulator.cc:145-148
+    Context.decode_frames      KmCodec::Decoder                          src/kmcodec.cc:54-72
+    Context.count_errors       lab::SourceSink::CntErr                   lib/lab/src/sourcesink.cc:29-47
+    Context.sim_generate/decode  one SNR point of Simulator::run_blocks   src/simulator.cc:112-168
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+__all__ = ["Context", "KmlError", "lib", "LIB_PATH", "BinaryLDPCCodec", "KMeans", "KmCodec"]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkmldpc_amd.so")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include", "kmldpc_amd.h")
+
+KML_DEVICE_PTRS = 1
+DIM_NAMES = ["M", "Ncol", "K", "cc_len", "Z", "E", "chk", "max_iter", "bits", "Kc", "S", "bp_lds"]
+
+
+class KmlError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libkmldpc_amd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise KmlError(f"{LIB_PATH} not built: run `make lib` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    P, I, D = C.c_void_p, C.c_int, C.c_double
+    PP = C.POINTER(C.c_void_p)
+    sig = {
+        "kml_abi_version": (I, []),
+        "kml_create": (I, [C.c_char_p, C.c_char_p, I, PP]),
+        "kml_create_explicit": (I, [C.c_char_p, C.c_char_p, I, I, I, I, I, I, PP]),
+        "kml_destroy": (None, [P]),
+        "kml_last_error": (C.c_char_p, [P]),
+        "kml_dims": (I, [P, P]),
+        "kml_code_perm": (I, [P, P]),
+        "kml_code_graph": (I, [P, P, P, P, P]),
+        "kml_constellation": (I, [P, P]),
+        "kml_encode": (I, [P, P, P, I]),
+        "kml_bp_decode": (I, [P, P, I, I, P, P, P, P, I]),
+        "kml_demap": (I, [P, P, P, D, I, P, I]),
+        "kml_kmeans": (I, [P, P, I, I, P, P, I]),
+        "kml_decode_frames": (I, [P, P, P, D, I, P, P, P, P, P, I]),
+        "kml_count_errors": (I, [P, P, P, I, P, I]),
+        "kml_sim_generate": (I, [P, D, C.c_uint64, C.c_uint64, I]),
+        "kml_sim_decode": (I, [P, D, I, P, I]),
+        "kml_sync": (I, [P]),
+        "kml_sim_frames": (I, [P, P, P, P]),
+        "kml_prof_enable": (I, [P, I]),
+        "kml_prof_reset": (I, [P]),
+        "kml_prof_read": (I, [P, C.c_char_p, P, P, P]),
+        "kml_math_probe": (I, [P, P, I, P]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def header_symbols():
+    """Function names declared by include/kmldpc_amd.h."""
+    import re
+    txt = open(INCLUDE).read()
+    return sorted(set(re.findall(r"\b(kml_[a-z0-9_]+)\s*\(", txt)))
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _f64(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if shape is not None:
+        a = a.reshape(shape)
+    return a
+
+
+class Context:
+    """One code + modem on one GPU (device < 0: host-only planner context)."""
+
+    def __init__(self, config=None, data_dir=None, device=0, *, matrix_file=None, modem_file=None, is5g=False,
+                 active=True, max_iter=20, metric_soft=False, metric_iter=5):
+        L = lib()
+        h = C.c_void_p()
+        if config is not None:
+            r = L.kml_create(os.fsencode(config), os.fsencode(data_dir) if data_dir else None, int(device),
+                             C.byref(h))
+        else:
+            if matrix_file is None or modem_file is None:
+                raise ValueError("need a config path or matrix_file + modem_file")
+            r = L.kml_create_explicit(os.fsencode(matrix_file), os.fsencode(modem_file), int(is5g), int(active),
+                                      int(max_iter), int(metric_soft), int(metric_iter), int(device), C.byref(h))
+        self._h = h
+        if r != 0:
+            msg = L.kml_last_error(h).decode() if h.value else "kml_create failed"
+            if h.value:
+                L.kml_destroy(h)
+            self._h = None
+            raise KmlError(f"kml_create: {msg} (code {r})")
+        d = np.zeros(len(DIM_NAMES), np.int32)
+        L.kml_dims(h, _p(d))
+        self.dims = {k: int(v) for k, v in zip(DIM_NAMES, d)}
+        for k, v in self.dims.items():
+            setattr(self, k, v)
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().kml_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _chk(self, r, what):
+        if r != 0:
+            raise KmlError(f"{what}: {lib().kml_last_error(self._h).decode()} (code {r})")
+
+    # ---- planner / host side
+    def perm(self):
+        p = np.zeros(self.Ncol, np.int32)
+        self._chk(lib().kml_code_perm(self._h, _p(p)), "kml_code_perm")
+        return p
+
+    def graph(self):
+        rp = np.zeros(self.M + 1, np.int32)
+        rc = np.zeros(self.E, np.int32)
+        cp = np.zeros(self.Ncol + 1, np.int32)
+        cs = np.zeros(self.E, np.int32)
+        self._chk(lib().kml_code_graph(self._h, _p(rp), _p(rc), _p(cp), _p(cs)), "kml_code_graph")
+        return rp, rc, cp, cs
+
+    def constellation(self):
+        pts = np.zeros(2 * self.Kc)
+        self._chk(lib().kml_constellation(self._h, _p(pts)), "kml_constellation")
+        return pts.reshape(-1, 2)
+
+    def encode(self, uu):
+        uu = np.ascontiguousarray(uu, np.uint8).reshape(-1, self.K)
+        cc = np.zeros((uu.shape[0], self.cc_len), np.uint8)
+        self._chk(lib().kml_encode(self._h, _p(uu), _p(cc), uu.shape[0]), "kml_encode")
+        return cc
+
+    # ---- GPU entry points
+    def bp_decode(self, p0, iter_count=None, cc_hat=False, syn=None):
+        """BinaryLDPCCodec::Decoder over a batch; returns dict(uu_hat, ret[, cc_hat, syn])."""
+        p0 = _f64(p0).reshape(-1, self.cc_len)
+        B = p0.shape[0]
+        it = self.max_iter if iter_count is None else int(iter_count)
+        uh = np.zeros((B, self.K), np.uint8)
+        ret = np.zeros(B, np.int32)
+        cch = np.zeros((B, self.Ncol), np.uint8) if cc_hat else None
+        if syn is not None:
+            syn = _f64(syn).reshape(B, self.M).copy()
+        self._chk(lib().kml_bp_decode(self._h, _p(p0), B, it, _p(uh), _p(ret), _p(cch), _p(syn), 0), "kml_bp_decode")
+        out = dict(uu_hat=uh, ret=ret)
+        if cc_hat:
+            out["cc_hat"] = cch
+        if syn is not None:
+            out["syn"] = syn
+        return out
+
+    def demap(self, y, h, var):
+        y = _f64(y).reshape(-1, self.S, 2)
+        B = y.shape[0]
+        h = _f64(h).reshape(B, 2)
+        p0 = np.zeros((B, self.cc_len))
+        self._chk(lib().kml_demap(self._h, _p(y), _p(h), float(var), B, _p(p0), 0), "kml_demap")
+        return p0
+
+    def kmeans(self, y, iters=20):
+        y = _f64(y).reshape(-1, self.S, 2)
+        B = y.shape[0]
+        hh = np.zeros((B, 2))
+        h4 = np.zeros((B, 4, 2))
+        self._chk(lib().kml_kmeans(self._h, _p(y), B, int(iters), _p(hh), _p(h4), 0), "kml_kmeans")
+        return hh, h4
+
+    def decode_frames(self, y, snr, true_h=None):
+        """KmCodec::Decoder: known channel if true_h is given, else the blind path."""
+        y = _f64(y).reshape(-1, self.S, 2)
+        B = y.shape[0]
+        th = None if true_h is None else _f64(true_h).reshape(B, 2)
+        uh = np.zeros((B, self.K), np.uint8)
+        ch = np.zeros(B, np.int32)
+        met = np.zeros((B, 4))
+        ret = np.zeros(B, np.int32)
+        hh = np.zeros((B, 2))
+        self._chk(lib().kml_decode_frames(self._h, _p(y), _p(th), float(snr), B, _p(uh), _p(ch), _p(met), _p(ret),
+                                          _p(hh), 0), "kml_decode_frames")
+        return dict(uu_hat=uh, chosen=ch, metrics=met, ret=ret, h_hat=hh)
+
+    def count_errors(self, uu, uu_hat):
+        uu = np.ascontiguousarray(uu, np.uint8).reshape(-1, self.K)
+        uh = np.ascontiguousarray(uu_hat, np.uint8).reshape(-1, self.K)
+        cnt = np.zeros(4, np.uint64)
+        self._chk(lib().kml_count_errors(self._h, _p(uu), _p(uh), uu.shape[0], _p(cnt), 0), "kml_count_errors")
+        return dict(zip(["err_bit", "err_blk", "tot_bit", "tot_blk"], [int(x) for x in cnt]))
+
+    def sim_generate(self, snr, B, seed=17, first_cw=0):
+        self._chk(lib().kml_sim_generate(self._h, float(snr), int(seed), int(first_cw), int(B)), "kml_sim_generate")
+
+    def sim_decode(self, snr, blind=False, sync=True):
+        if not sync:
+            self._chk(lib().kml_sim_decode(self._h, float(snr), int(blind), None, 0), "kml_sim_decode")
+            return None
+        cnt = np.zeros(8, np.uint64)
+        self._chk(lib().kml_sim_decode(self._h, float(snr), int(blind), _p(cnt), 1), "kml_sim_decode")
+        return dict(zip(["err_bit", "err_blk", "tot_bit", "tot_blk", "vn_phases", "cn_phases", "converged"],
+                        [int(x) for x in cnt[:7]]))
+
+    def sync(self):
+        self._chk(lib().kml_sync(self._h), "kml_sync")
+
+    def sim_frames(self, B):
+        uu = np.zeros((B, self.K), np.uint8)
+        y = np.zeros((B, self.S, 2))
+        h = np.zeros((B, 2))
+        self._chk(lib().kml_sim_frames(self._h, _p(uu), _p(y), _p(h)), "kml_sim_frames")
+        return uu, y, h
+
+    def prof_enable(self, on=True):
+        self._chk(lib().kml_prof_enable(self._h, int(on)), "kml_prof_enable")
+
+    def prof_reset(self):
+        self._chk(lib().kml_prof_reset(self._h), "kml_prof_reset")
+
+    def prof_read(self, stage):
+        n = np.zeros(1, np.int64)
+        ms = np.zeros(1)
+        by = np.zeros(1)
+        self._chk(lib().kml_prof_read(self._h, stage.encode(), _p(n), _p(ms), _p(by)), "kml_prof_read")
+        return dict(launches=int(n[0]), ms=float(ms[0]), bytes=float(by[0]))
+
+    def math_probe(self, x):
+        x = _f64(x).reshape(-1, 4)
+        out = np.zeros_like(x)
+        self._chk(lib().kml_math_probe(self._h, _p(x), x.shape[0], _p(out)), "kml_math_probe")
+        return out
+
+
+# ---------------------------------------------------------------------------
+# Reference-shaped facades (same method names and argument meaning as the C++
+# classes, batched along a leading axis).
+
+class BinaryLDPCCodec:
+    """lab::BinaryLDPCCodec / lab::Binary5GLDPCCodec (lib/lab/include/binaryldpccodec.h:11-56)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def Decoder(self, M2V, uu_hat, iter_count):
+        """Decodes M2V[B, cc_len]; fills uu_hat[B, K]; returns the per-codeword return values."""
+        r = self.ctx.bp_decode(M2V, iter_count)
+        uu_hat[...] = r["uu_hat"].reshape(uu_hat.shape)
+        return r["ret"]
+
+    def Encoder(self, uu, cc):
+        cc[...] = self.ctx.encode(uu).reshape(cc.shape)
+
+    def code_dim(self):
+        return self.ctx.K
+
+    def code_len(self):
+        return self.ctx.cc_len
+
+    def num_row(self):
+        return self.ctx.M
+
+    def max_iter(self):
+        return self.ctx.max_iter
+
+
+class KMeans:
+    """kmldpc::KMeans (include/kmeans.h:12-32), batched: data[B, S, 2]."""
+
+    def __init__(self, ctx, data, iters=20):
+        self.ctx, self.data, self.iters = ctx, data, iters
+        self._hh = None
+
+    def Run(self):
+        self._hh, self._h4 = self.ctx.kmeans(self.data, self.iters)
+
+    def h_hat(self):
+        """clusters()[0] / constellations[0] (src/simulator.cc:145)."""
+        return self._hh
+
+    def h_hats(self):
+        """the 4 phase candidates (src/simulator.cc:146-148)."""
+        return self._h4
+
+
+class KmCodec:
+    """KmCodec (include/kmcodec.h:16-53): blind or known-channel decode."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def Decoder(self, y, snr, uu_hat, true_h=None):
+        r = self.ctx.decode_frames(y, snr, true_h)
+        uu_hat[...] = r["uu_hat"].reshape(uu_hat.shape)
+        return r
+
+    def uu_len(self):
+        return self.ctx.K
+
+    def cc_len(self):
+        return self.ctx.cc_len

@@ -1,0 +1,758 @@
+// capi.cpp — the C ABI (include/kmldpc_amd.h) over the host planner and the
+// gfx950 kernels.  One context = one GPU + one HIP stream + one code/modem.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/kmldpc_amd.h"
+#include "code.hpp"
+#include "config.hpp"
+#include "kernels.hpp"
+#include "modem.hpp"
+
+namespace {
+
+struct DBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 256);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T *as() const {
+    return reinterpret_cast<T *>(p);
+  }
+};
+
+struct Pending {
+  std::string stage;
+  hipEvent_t ev0, ev1;
+  int cnt_slot;  // counter-arena slot for "bp" launches (-1 otherwise)
+  double fixed_bytes;
+};
+
+struct Stat {
+  int64_t launches = 0;
+  double ms = 0, bytes = 0;
+};
+
+constexpr int kArenaSlots = 1024;
+
+}  // namespace
+
+struct kml_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  kml::RunConfig rc;
+  kml::LdpcCode code;
+  kml::Modem modem;
+  kml::DevCode dc{};
+  double rot[8];
+  // resident constants
+  DBuf d_graph, d_cons;
+  DBuf d_arena;  // kArenaSlots x CNT_N counters
+  int arena_next = 0;
+  DBuf d_queue, d_gslots;
+  long long gslots_cap = 0;
+  // workspaces
+  DBuf w_y, w_h, w_h4, w_hhat, w_p0, w_uu, w_uh, w_ret, w_cch, w_syn, w_sel, w_met, w_pc, w_cnt;
+  // resident simulation frames
+  DBuf s_uu, s_cc, s_y, s_h;
+  int sim_B = 0;
+  double sim_snr = 0;
+  // profiling
+  bool prof = false;
+  std::vector<Pending> pend;
+  std::map<std::string, Stat> stats;
+  std::string err;
+};
+
+namespace {
+
+int fail(kml_ctx *c, int code, const std::string &msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hip_fail(kml_ctx *c, hipError_t e, const char *what) {
+  return fail(c, KML_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(ctx, expr, what)                       \
+  do {                                                \
+    hipError_t _e = (expr);                           \
+    if (_e != hipSuccess) return hip_fail(ctx, _e, what); \
+  } while (0)
+
+int upload_code(kml_ctx *c) {
+  const kml::LdpcCode &L = c->code;
+  // pack all int32 arrays + enc words into one allocation
+  std::vector<size_t> off;
+  size_t bytes = 0;
+  auto reserve = [&](size_t n) {
+    bytes = (bytes + 255) & ~size_t(255);
+    off.push_back(bytes);
+    bytes += n;
+  };
+  reserve(L.row_ptr.size() * 4);
+  reserve(L.row_col.size() * 4);
+  reserve(L.col_ptr.size() * 4);
+  reserve(L.col_slot.size() * 4);
+  reserve(L.vn_order.size() * 4);
+  reserve(L.cn_order.size() * 4);
+  reserve(std::max<size_t>(L.enc_info.size(), 1) * 8);
+  HIPCHK(c, c->d_graph.ensure(bytes), "hipMalloc(graph)");
+  std::vector<unsigned char> host(bytes, 0);
+  auto put = [&](int i, const void *src, size_t n) {
+    if (n) memcpy(host.data() + off[i], src, n);
+  };
+  put(0, L.row_ptr.data(), L.row_ptr.size() * 4);
+  put(1, L.row_col.data(), L.row_col.size() * 4);
+  put(2, L.col_ptr.data(), L.col_ptr.size() * 4);
+  put(3, L.col_slot.data(), L.col_slot.size() * 4);
+  put(4, L.vn_order.data(), L.vn_order.size() * 4);
+  put(5, L.cn_order.data(), L.cn_order.size() * 4);
+  put(6, L.enc_info.data(), L.enc_info.size() * 8);
+  HIPCHK(c, hipMemcpy(c->d_graph.p, host.data(), bytes, hipMemcpyHostToDevice), "upload graph");
+  unsigned char *base = c->d_graph.as<unsigned char>();
+  kml::DevCode &d = c->dc;
+  d.row_ptr = reinterpret_cast<const int32_t *>(base + off[0]);
+  d.row_col = reinterpret_cast<const int32_t *>(base + off[1]);
+  d.col_ptr = reinterpret_cast<const int32_t *>(base + off[2]);
+  d.col_slot = reinterpret_cast<const int32_t *>(base + off[3]);
+  d.vn_order = reinterpret_cast<const int32_t *>(base + off[4]);
+  d.cn_order = reinterpret_cast<const int32_t *>(base + off[5]);
+  d.enc_info = reinterpret_cast<const uint64_t *>(base + off[6]);
+  d.M = L.M;
+  d.N = L.N;
+  d.E = L.E;
+  d.K = L.K;
+  d.cc_len = L.cc_len;
+  d.punct = L.punct;
+  d.info_off = L.info_off;
+  d.chk = L.chk;
+  d.Kw = L.Kw;
+  d.dv_max = L.dv_max;
+  d.dc_max = L.dc_max;
+  d.is5g = L.is5g ? 1 : 0;
+  d.active = L.active ? 1 : 0;
+
+  HIPCHK(c, c->d_cons.ensure(sizeof(double) * (c->modem.pts.size() + 8)), "hipMalloc(cons)");
+  kml::rotation_factors(c->rot);
+  std::vector<double> cr(c->modem.pts);
+  cr.insert(cr.end(), c->rot, c->rot + 8);
+  HIPCHK(c, hipMemcpy(c->d_cons.p, cr.data(), sizeof(double) * cr.size(), hipMemcpyHostToDevice), "upload cons");
+  HIPCHK(c, c->d_arena.ensure(sizeof(unsigned long long) * kml::CNT_N * kArenaSlots), "hipMalloc(counters)");
+  HIPCHK(c, c->d_queue.ensure(256), "hipMalloc(queue)");
+  const long long need = kml::bp_gslots_needed(d);
+  if (need > 0) {
+    HIPCHK(c, c->d_gslots.ensure((size_t)need * sizeof(double2)), "hipMalloc(gslots)");
+    c->gslots_cap = need;
+  }
+  return KML_OK;
+}
+
+int finish_create(kml_ctx *c) {
+  std::string err;
+  if (!c->code.load(c->rc.matrix_file, c->rc.is5g, c->rc.active, false, err)) return fail(c, KML_E_IO, err);
+  if (!c->modem.load(c->rc.modem_file, err)) return fail(c, KML_E_IO, err);
+  if (c->code.cc_len % c->modem.bits != 0)  // modemlinearsystem.cc:7-12
+    return fail(c, KML_E_ARG, "(cc_len = " + std::to_string(c->code.cc_len) + ") % (input_len = " +
+                                  std::to_string(c->modem.bits) + ") != 0");
+  if (c->modem.bits != 1 && c->modem.bits != 2 && c->modem.bits != 3 && c->modem.bits != 4 && c->modem.bits != 6)
+    return fail(c, KML_E_UNSUP, "bits per symbol must be 1, 2, 3, 4 or 6");
+  if (c->device < 0) {  // host-only context: planner + encoder, no GPU
+    kml::rotation_factors(c->rot);
+    return KML_OK;
+  }
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+  return upload_code(c);
+}
+
+// ---- profiling helpers
+int next_slot(kml_ctx *c) {
+  int s = c->arena_next;
+  c->arena_next = (c->arena_next + 1) % kArenaSlots;
+  return s;
+}
+unsigned long long *slot_ptr(kml_ctx *c, int s) { return c->d_arena.as<unsigned long long>() + (size_t)s * kml::CNT_N; }
+
+struct Timer {
+  kml_ctx *c;
+  Pending p;
+  bool on;
+  Timer(kml_ctx *ctx, const char *stage, int slot, double bytes) : c(ctx), on(ctx->prof) {
+    if (!on) return;
+    p.stage = stage;
+    p.cnt_slot = slot;
+    p.fixed_bytes = bytes;
+    hipEventCreate(&p.ev0);
+    hipEventCreate(&p.ev1);
+    hipEventRecord(p.ev0, c->stream);
+  }
+  void stop() {
+    if (!on) return;
+    hipEventRecord(p.ev1, c->stream);
+    c->pend.push_back(p);
+    on = false;
+  }
+};
+
+void drain_profile(kml_ctx *c) {
+  if (c->pend.empty()) return;
+  hipStreamSynchronize(c->stream);
+  for (auto &p : c->pend) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, p.ev0, p.ev1);
+    Stat &s = c->stats[p.stage];
+    s.launches++;
+    s.ms += ms;
+    double bytes = p.fixed_bytes;
+    if (p.cnt_slot >= 0) {
+      unsigned long long h[kml::CNT_N];
+      hipMemcpy(h, slot_ptr(c, p.cnt_slot), sizeof(h), hipMemcpyDeviceToHost);
+      const double E = c->code.E, N = c->code.N;
+      bytes += (double)h[kml::CNT_VN_PHASES] * (24.0 * E + 9.0 * N) + (double)h[kml::CNT_CN_PHASES] * 24.0 * E;
+    }
+    s.bytes += bytes;
+    hipEventDestroy(p.ev0);
+    hipEventDestroy(p.ev1);
+  }
+  c->pend.clear();
+}
+
+// Launch BP over n entries with a fresh counter slot; returns the slot.
+int run_bp(kml_ctx *c, kml::BpLaunch a, int &slot_out) {
+  const int slot = next_slot(c);
+  HIPCHK(c, hipMemsetAsync(slot_ptr(c, slot), 0, sizeof(unsigned long long) * kml::CNT_N, c->stream), "memset");
+  a.counters = slot_ptr(c, slot);
+  a.gslots = c->d_gslots.as<double2>();
+  a.gslots_cap = c->gslots_cap;
+  a.queue = c->d_queue.as<unsigned int>();
+  Timer t(c, "bp", slot, (double)a.B * 8.0 * c->code.cc_len);
+  const char *msg = nullptr;
+  hipError_t e = kml::launch_bp(c->dc, a, c->stream, &msg);
+  t.stop();
+  if (e != hipSuccess) return msg ? fail(c, KML_E_UNSUP, msg) : hip_fail(c, e, "bp launch");
+  slot_out = slot;
+  return KML_OK;
+}
+
+// Stage a host or device input; returns a device pointer.
+template <class T>
+int stage_in(kml_ctx *c, DBuf &buf, const T *src, size_t n, int flags, const T *&dev) {
+  if (flags & KML_DEVICE_PTRS) {
+    dev = src;
+    return KML_OK;
+  }
+  HIPCHK(c, buf.ensure(n * sizeof(T)), "hipMalloc(workspace)");
+  if (n) HIPCHK(c, hipMemcpyAsync(buf.p, src, n * sizeof(T), hipMemcpyHostToDevice, c->stream), "H2D");
+  dev = buf.as<T>();
+  return KML_OK;
+}
+
+template <class T>
+int stage_out_ptr(kml_ctx *c, DBuf &buf, T *dst, size_t n, int flags, T *&dev) {
+  if (!dst) {
+    dev = nullptr;
+    return KML_OK;
+  }
+  if (flags & KML_DEVICE_PTRS) {
+    dev = dst;
+    return KML_OK;
+  }
+  HIPCHK(c, buf.ensure(n * sizeof(T)), "hipMalloc(workspace)");
+  dev = buf.as<T>();
+  return KML_OK;
+}
+
+template <class T>
+int copy_out(kml_ctx *c, T *dst, const T *dev, size_t n, int flags) {
+  if (!dst || (flags & KML_DEVICE_PTRS) || n == 0) return KML_OK;
+  HIPCHK(c, hipMemcpyAsync(dst, dev, n * sizeof(T), hipMemcpyDeviceToHost, c->stream), "D2H");
+  return KML_OK;
+}
+
+int sync(kml_ctx *c) {
+  HIPCHK(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  return KML_OK;
+}
+
+int need_gpu(kml_ctx *c) {
+  if (c->device < 0 || !c->stream) return fail(c, KML_E_ARG, "host-only context (device < 0): no GPU operations");
+  return KML_OK;
+}
+
+#define TRY(x)            \
+  do {                    \
+    int _r = (x);         \
+    if (_r != KML_OK) return _r; \
+  } while (0)
+
+// Receive path shared by kml_decode_frames and kml_sim_decode: y/h are
+// device pointers.  Produces p0 selection + BP.
+int receive(kml_ctx *c, const double2 *y, const double2 *true_h, double snr, int B, uint8_t *d_uh, int32_t *d_chosen,
+            double *d_met, int32_t *d_ret, double2 *d_hhat, const uint64_t *ref_bits, int &bp_slot) {
+  double var, sigma, ns;
+  kml::channel_constants(snr, var, sigma, ns);
+  const int S = c->code.cc_len / c->modem.bits;
+  const double *cons = c->d_cons.as<double>();
+  const double *rot = cons + c->modem.pts.size();
+  const size_t cc = (size_t)c->code.cc_len;
+  kml::BpLaunch a;
+  a.B = B;
+  a.iter_count = c->rc.max_iter;
+  a.max_iter = c->rc.max_iter;
+  a.uu_hat = d_uh;
+  a.ret = d_ret;
+  a.ref_bits = ref_bits;
+  if (true_h) {  // known channel (simulator.cc:132-133)
+    HIPCHK(c, c->w_p0.ensure(sizeof(double) * cc * B), "hipMalloc(p0)");
+    Timer t(c, "demap", -1, (double)B * S * (16.0 + 8.0 * c->modem.bits));
+    HIPCHK(c, kml::launch_demap(c->modem.bits, cons, y, S, 1, true_h, 1, nullptr, var, B, c->w_p0.as<double>(), c->stream),
+           "demap");
+    t.stop();
+    a.p0 = c->w_p0.as<double>();
+    a.p0_stride = (long long)cc;
+    return run_bp(c, a, bp_slot);
+  }
+  // blind: k-means (simulator.cc:136-148)
+  HIPCHK(c, c->w_h4.ensure(sizeof(double2) * 4 * B), "hipMalloc(h4)");
+  double2 *hh = d_hhat;
+  if (!hh) {
+    HIPCHK(c, c->w_hhat.ensure(sizeof(double2) * B), "hipMalloc(hhat)");
+    hh = c->w_hhat.as<double2>();
+  }
+  {
+    Timer t(c, "kmeans", -1, (double)B * S * 16.0);
+    HIPCHK(c, kml::launch_kmeans(c->modem.Kc, cons, rot, y, S, 20, B, hh, c->w_h4.as<double2>(), c->stream), "kmeans");
+    t.stop();
+  }
+  int32_t *chosen = d_chosen;
+  double *met = d_met;
+  if (!chosen) {
+    HIPCHK(c, c->w_sel.ensure(sizeof(int32_t) * B), "hipMalloc(sel)");
+    chosen = c->w_sel.as<int32_t>();
+  }
+  if (!met) {
+    HIPCHK(c, c->w_met.ensure(sizeof(double) * 4 * B), "hipMalloc(met)");
+    met = c->w_met.as<double>();
+  }
+  if (c->rc.metric_soft)
+    return fail(c, KML_E_UNSUP, "[xcodec] metric_type = true (soft syndrome metric) is not implemented yet");
+  if (!c->code.is5g) {  // hard metric on the demapper output (kmcodec.cc:109-117)
+    Timer t(c, "metric", -1, (double)B * S * 16.0);
+    HIPCHK(c, kml::launch_cand_metric(c->dc, c->modem.bits, cons, y, S, c->w_h4.as<double2>(), var, B, nullptr, met,
+                                      chosen, c->stream),
+           "cand_metric");
+    t.stop();
+    HIPCHK(c, c->w_p0.ensure(sizeof(double) * cc * B), "hipMalloc(p0)");
+    Timer t2(c, "demap", -1, (double)B * S * (16.0 + 8.0 * c->modem.bits));
+    HIPCHK(c, kml::launch_demap(c->modem.bits, cons, y, S, 1, c->w_h4.as<double2>(), 4, chosen, var, B,
+                                c->w_p0.as<double>(), c->stream),
+           "demap");
+    t2.stop();
+    a.p0 = c->w_p0.as<double>();
+    a.p0_stride = (long long)cc;
+    return run_bp(c, a, bp_slot);
+  }
+  // 5G: metric = parity count after metric_iter BP iterations (kmcodec.cc:157-160)
+  HIPCHK(c, c->w_p0.ensure(sizeof(double) * cc * 4 * B), "hipMalloc(p0)");
+  HIPCHK(c, c->w_pc.ensure(sizeof(int32_t) * 4 * B), "hipMalloc(pc)");
+  {
+    Timer t(c, "demap", -1, 4.0 * B * S * (16.0 + 8.0 * c->modem.bits));
+    HIPCHK(c, kml::launch_demap(c->modem.bits, cons, y, S, 4, c->w_h4.as<double2>(), 1, nullptr, var, 4 * B,
+                                c->w_p0.as<double>(), c->stream),
+           "demap4");
+    t.stop();
+  }
+  kml::BpLaunch m;
+  m.B = 4 * B;
+  m.iter_count = c->rc.metric_iter;
+  m.max_iter = c->rc.max_iter;
+  m.p0 = c->w_p0.as<double>();
+  m.p0_stride = (long long)cc;
+  m.parity_cnt = c->w_pc.as<int32_t>();
+  int mslot = 0;
+  TRY(run_bp(c, m, mslot));
+  HIPCHK(c, kml::launch_select(c->w_pc.as<int32_t>(), B, met, chosen, c->stream), "select");
+  a.p0 = c->w_p0.as<double>();
+  a.p0_stride = (long long)cc * 4;
+  a.p0_sel = chosen;
+  a.p0_sel_stride = (long long)cc;
+  return run_bp(c, a, bp_slot);
+}
+
+}  // namespace
+
+extern "C" {
+
+int kml_abi_version(void) { return KML_ABI_VERSION; }
+
+int kml_create(const char *config_toml, const char *data_dir, int device, kml_ctx **out) {
+  if (!out || !config_toml) return KML_E_ARG;
+  *out = nullptr;
+  kml_ctx *c = new kml_ctx();
+  c->device = device;
+  std::string err;
+  if (!kml::load_run_config(config_toml, data_dir ? data_dir : "", c->rc, err)) {
+    c->err = err;
+    *out = c;  // keep the context so kml_last_error can report
+    return KML_E_IO;
+  }
+  int r = finish_create(c);
+  *out = c;
+  return r;
+}
+
+int kml_create_explicit(const char *matrix_file, const char *modem_file, int is5g, int active, int max_iter,
+                        int metric_soft, int metric_iter, int device, kml_ctx **out) {
+  if (!out || !matrix_file || !modem_file) return KML_E_ARG;
+  kml_ctx *c = new kml_ctx();
+  c->device = device;
+  c->rc.matrix_file = matrix_file;
+  c->rc.modem_file = modem_file;
+  c->rc.is5g = is5g != 0;
+  c->rc.active = active != 0;
+  c->rc.max_iter = max_iter;
+  c->rc.metric_soft = metric_soft != 0;
+  c->rc.metric_iter = metric_iter;
+  int r = finish_create(c);
+  *out = c;
+  return r;
+}
+
+void kml_destroy(kml_ctx *c) {
+  if (!c) return;
+  if (c->stream && c->device >= 0) {
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    drain_profile(c);
+    for (DBuf *b : {&c->d_graph, &c->d_cons, &c->d_arena, &c->d_queue, &c->d_gslots, &c->w_y, &c->w_h, &c->w_h4,
+                    &c->w_hhat, &c->w_p0, &c->w_uu, &c->w_uh, &c->w_ret, &c->w_cch, &c->w_syn, &c->w_sel, &c->w_met,
+                    &c->w_pc, &c->w_cnt, &c->s_uu, &c->s_cc, &c->s_y, &c->s_h})
+      b->release();
+    hipStreamDestroy(c->stream);
+  }
+  delete c;
+}
+
+const char *kml_last_error(const kml_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int kml_dims(const kml_ctx *c, int32_t *d) {
+  if (!c || !d) return KML_E_ARG;
+  const kml::LdpcCode &L = c->code;
+  d[KML_DIM_M] = L.M;
+  d[KML_DIM_NCOL] = L.N;
+  d[KML_DIM_K] = L.K;
+  d[KML_DIM_CCLEN] = L.cc_len;
+  d[KML_DIM_Z] = L.Z;
+  d[KML_DIM_E] = L.E;
+  d[KML_DIM_CHK] = L.chk;
+  d[KML_DIM_MAXITER] = c->rc.max_iter;
+  d[KML_DIM_BITS] = c->modem.bits;
+  d[KML_DIM_KC] = c->modem.Kc;
+  d[KML_DIM_S] = c->modem.bits ? L.cc_len / c->modem.bits : 0;
+  kml::DevCode tmp{};
+  tmp.E = L.E;
+  tmp.N = L.N;
+  d[KML_DIM_BP_LDS] = kml::bp_uses_lds(tmp) ? 1 : 0;
+  return KML_OK;
+}
+
+int kml_code_perm(const kml_ctx *c, int32_t *perm) {
+  if (!c || !perm) return KML_E_ARG;
+  memcpy(perm, c->code.perm.data(), sizeof(int32_t) * c->code.perm.size());
+  return KML_OK;
+}
+
+int kml_code_graph(const kml_ctx *c, int32_t *rp, int32_t *rc, int32_t *cp, int32_t *cs) {
+  if (!c) return KML_E_ARG;
+  const kml::LdpcCode &L = c->code;
+  if (rp) memcpy(rp, L.row_ptr.data(), 4 * L.row_ptr.size());
+  if (rc) memcpy(rc, L.row_col.data(), 4 * L.row_col.size());
+  if (cp) memcpy(cp, L.col_ptr.data(), 4 * L.col_ptr.size());
+  if (cs) memcpy(cs, L.col_slot.data(), 4 * L.col_slot.size());
+  return KML_OK;
+}
+
+int kml_constellation(const kml_ctx *c, double *pts) {
+  if (!c || !pts) return KML_E_ARG;
+  memcpy(pts, c->modem.pts.data(), sizeof(double) * c->modem.pts.size());
+  return KML_OK;
+}
+
+int kml_encode(const kml_ctx *c, const uint8_t *uu, uint8_t *cc, int B) {
+  if (!c || !uu || !cc || B < 0) return KML_E_ARG;
+  for (int b = 0; b < B; b++) c->code.encode(uu + (size_t)b * c->code.K, cc + (size_t)b * c->code.cc_len);
+  return KML_OK;
+}
+
+int kml_bp_decode(kml_ctx *c, const double *p0, int B, int iter_count, uint8_t *uu_hat, int32_t *ret, uint8_t *cc_hat,
+                  double *syn, int flags) {
+  if (!c || !p0 || B < 0 || iter_count < 0) return fail(c, KML_E_ARG, "kml_bp_decode: bad argument");
+  if (B == 0) return KML_OK;
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const kml::LdpcCode &L = c->code;
+  const double *d_p0;
+  TRY(stage_in(c, c->w_p0, p0, (size_t)B * L.cc_len, flags, d_p0));
+  uint8_t *d_uh, *d_cch;
+  int32_t *d_ret;
+  double *d_syn;
+  TRY(stage_out_ptr(c, c->w_uh, uu_hat, (size_t)B * L.K, flags, d_uh));
+  TRY(stage_out_ptr(c, c->w_ret, ret, (size_t)B, flags, d_ret));
+  TRY(stage_out_ptr(c, c->w_cch, cc_hat, (size_t)B * L.N, flags, d_cch));
+  TRY(stage_out_ptr(c, c->w_syn, syn, (size_t)B * L.M, flags, d_syn));
+  // syndrom_soft semantics: rows not rewritten keep the caller's values
+  if (syn && !(flags & KML_DEVICE_PTRS))
+    HIPCHK(c, hipMemcpyAsync(d_syn, syn, sizeof(double) * B * L.M, hipMemcpyHostToDevice, c->stream), "H2D syn");
+  kml::BpLaunch a;
+  a.B = B;
+  a.iter_count = iter_count;
+  a.max_iter = c->rc.max_iter;
+  a.p0 = d_p0;
+  a.p0_stride = L.cc_len;
+  a.uu_hat = d_uh;
+  a.ret = d_ret;
+  a.cc_hat = d_cch;
+  a.syn = d_syn;
+  int slot;
+  TRY(run_bp(c, a, slot));
+  TRY(copy_out(c, uu_hat, d_uh, (size_t)B * L.K, flags));
+  TRY(copy_out(c, ret, d_ret, (size_t)B, flags));
+  TRY(copy_out(c, cc_hat, d_cch, (size_t)B * L.N, flags));
+  TRY(copy_out(c, syn, d_syn, (size_t)B * L.M, flags));
+  return sync(c);
+}
+
+int kml_demap(kml_ctx *c, const double *y, const double *h, double var, int B, double *p0, int flags) {
+  if (!c || !y || !h || !p0 || B < 0) return fail(c, KML_E_ARG, "kml_demap: bad argument");
+  if (B == 0) return KML_OK;
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const int S = c->code.cc_len / c->modem.bits;
+  const double *d_y, *d_h;
+  TRY(stage_in(c, c->w_y, y, (size_t)B * S * 2, flags, d_y));
+  TRY(stage_in(c, c->w_h, h, (size_t)B * 2, flags, d_h));
+  double *d_p0;
+  TRY(stage_out_ptr(c, c->w_p0, p0, (size_t)B * c->code.cc_len, flags, d_p0));
+  Timer t(c, "demap", -1, (double)B * S * (16.0 + 8.0 * c->modem.bits));
+  HIPCHK(c, kml::launch_demap(c->modem.bits, c->d_cons.as<double>(), reinterpret_cast<const double2 *>(d_y), S, 1,
+                              reinterpret_cast<const double2 *>(d_h), 1, nullptr, var, B, d_p0, c->stream),
+         "demap");
+  t.stop();
+  TRY(copy_out(c, p0, d_p0, (size_t)B * c->code.cc_len, flags));
+  return sync(c);
+}
+
+int kml_kmeans(kml_ctx *c, const double *y, int B, int iters, double *h_hat, double *h4, int flags) {
+  if (!c || !y || B < 0 || iters < 0) return fail(c, KML_E_ARG, "kml_kmeans: bad argument");
+  if (B == 0) return KML_OK;
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const int S = c->code.cc_len / c->modem.bits;
+  const double *d_y;
+  TRY(stage_in(c, c->w_y, y, (size_t)B * S * 2, flags, d_y));
+  double *d_hh, *d_h4;
+  HIPCHK(c, c->w_hhat.ensure(sizeof(double2) * B), "hipMalloc");
+  HIPCHK(c, c->w_h4.ensure(sizeof(double2) * 4 * B), "hipMalloc");
+  d_hh = (h_hat && (flags & KML_DEVICE_PTRS)) ? h_hat : c->w_hhat.as<double>();
+  d_h4 = (h4 && (flags & KML_DEVICE_PTRS)) ? h4 : c->w_h4.as<double>();
+  const double *cons = c->d_cons.as<double>();
+  Timer t(c, "kmeans", -1, (double)B * S * 16.0);
+  HIPCHK(c, kml::launch_kmeans(c->modem.Kc, cons, cons + c->modem.pts.size(), reinterpret_cast<const double2 *>(d_y), S,
+                               iters, B, reinterpret_cast<double2 *>(d_hh), reinterpret_cast<double2 *>(d_h4),
+                               c->stream),
+         "kmeans");
+  t.stop();
+  TRY(copy_out(c, h_hat, (const double *)d_hh, (size_t)B * 2, flags));
+  TRY(copy_out(c, h4, (const double *)d_h4, (size_t)B * 8, flags));
+  return sync(c);
+}
+
+int kml_decode_frames(kml_ctx *c, const double *y, const double *true_h, double snr, int B, uint8_t *uu_hat,
+                      int32_t *chosen, double *metrics, int32_t *ret, double *h_hat, int flags) {
+  if (!c || !y || !uu_hat || B < 0) return fail(c, KML_E_ARG, "kml_decode_frames: bad argument");
+  if (B == 0) return KML_OK;
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const int S = c->code.cc_len / c->modem.bits;
+  const double *d_y, *d_h = nullptr;
+  TRY(stage_in(c, c->w_y, y, (size_t)B * S * 2, flags, d_y));
+  if (true_h) TRY(stage_in(c, c->w_h, true_h, (size_t)B * 2, flags, d_h));
+  uint8_t *d_uh;
+  int32_t *d_ch, *d_ret;
+  double *d_met, *d_hh;
+  TRY(stage_out_ptr(c, c->w_uh, uu_hat, (size_t)B * c->code.K, flags, d_uh));
+  TRY(stage_out_ptr(c, c->w_sel, chosen, (size_t)B, flags, d_ch));
+  TRY(stage_out_ptr(c, c->w_met, metrics, (size_t)B * 4, flags, d_met));
+  TRY(stage_out_ptr(c, c->w_ret, ret, (size_t)B, flags, d_ret));
+  TRY(stage_out_ptr(c, c->w_hhat, h_hat, (size_t)B * 2, flags, d_hh));
+  int slot;
+  TRY(receive(c, reinterpret_cast<const double2 *>(d_y), reinterpret_cast<const double2 *>(d_h), snr, B, d_uh, d_ch,
+              d_met, d_ret, reinterpret_cast<double2 *>(d_hh), nullptr, slot));
+  if (true_h) {  // single candidate: chosen = 0, metrics unset (kmcodec.cc:66-67)
+    if (chosen && !(flags & KML_DEVICE_PTRS)) memset(chosen, 0, sizeof(int32_t) * B);
+    if (metrics && !(flags & KML_DEVICE_PTRS)) memset(metrics, 0, sizeof(double) * 4 * B);
+    if (h_hat && !(flags & KML_DEVICE_PTRS)) memset(h_hat, 0, sizeof(double) * 2 * B);
+  } else {
+    TRY(copy_out(c, chosen, d_ch, (size_t)B, flags));
+    TRY(copy_out(c, metrics, d_met, (size_t)B * 4, flags));
+    TRY(copy_out(c, h_hat, d_hh, (size_t)B * 2, flags));
+  }
+  TRY(copy_out(c, uu_hat, d_uh, (size_t)B * c->code.K, flags));
+  TRY(copy_out(c, ret, d_ret, (size_t)B, flags));
+  return sync(c);
+}
+
+int kml_count_errors(kml_ctx *c, const uint8_t *uu, const uint8_t *uu_hat, int B, uint64_t *counters, int flags) {
+  if (!c || !uu || !uu_hat || !counters || B < 0) return fail(c, KML_E_ARG, "kml_count_errors: bad argument");
+  if (B == 0) return KML_OK;
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const size_t n = (size_t)B * c->code.K;
+  const uint8_t *d_uu, *d_uh;
+  TRY(stage_in(c, c->w_uu, uu, n, flags, d_uu));
+  TRY(stage_in(c, c->w_uh, uu_hat, n, flags, d_uh));
+  HIPCHK(c, c->w_cnt.ensure(sizeof(unsigned long long) * kml::CNT_N), "hipMalloc");
+  HIPCHK(c, hipMemsetAsync(c->w_cnt.p, 0, sizeof(unsigned long long) * kml::CNT_N, c->stream), "memset");
+  HIPCHK(c, kml::launch_count_bytes(d_uu, d_uh, c->code.K, B, c->w_cnt.as<unsigned long long>(), c->stream), "count");
+  unsigned long long h[kml::CNT_N];
+  HIPCHK(c, hipMemcpyAsync(h, c->w_cnt.p, sizeof(h), hipMemcpyDeviceToHost, c->stream), "D2H");
+  TRY(sync(c));
+  for (int i = 0; i < 4; i++) counters[i] += h[i];
+  return KML_OK;
+}
+
+int kml_sim_generate(kml_ctx *c, double snr, uint64_t seed, uint64_t first_cw, int B) {
+  if (!c || B < 0) return fail(c, KML_E_ARG, "kml_sim_generate: bad argument");
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const kml::LdpcCode &L = c->code;
+  const int S = L.cc_len / c->modem.bits;
+  const int Cw = (L.cc_len + 63) / 64;
+  HIPCHK(c, c->s_uu.ensure(sizeof(uint64_t) * (size_t)B * L.Kw), "hipMalloc(sim uu)");
+  HIPCHK(c, c->s_cc.ensure(sizeof(uint64_t) * (size_t)B * Cw), "hipMalloc(sim cc)");
+  HIPCHK(c, c->s_y.ensure(sizeof(double2) * (size_t)B * S), "hipMalloc(sim y)");
+  HIPCHK(c, c->s_h.ensure(sizeof(double2) * (size_t)B), "hipMalloc(sim h)");
+  double var, sigma, ns;
+  kml::channel_constants(snr, var, sigma, ns);
+  kml::FrameLaunch f;
+  f.B = B;
+  f.seed = seed;
+  f.first_cw = first_cw;
+  f.noise_scale = ns;
+  f.uu_bits = c->s_uu.as<uint64_t>();
+  f.cc_bits = c->s_cc.as<uint64_t>();
+  f.y = c->s_y.as<double2>();
+  f.h = c->s_h.as<double2>();
+  Timer t(c, "framegen", -1, 0.0);
+  HIPCHK(c, kml::launch_framegen(c->dc, c->modem.bits, c->d_cons.as<double>(), f, c->stream), "framegen");
+  t.stop();
+  c->sim_B = B;
+  c->sim_snr = snr;
+  return sync(c);
+}
+
+int kml_sim_decode(kml_ctx *c, double snr, int blind, uint64_t *counters, int do_sync) {
+  if (!c) return KML_E_ARG;
+  if (!do_sync && counters) return fail(c, KML_E_ARG, "counters need sync != 0");
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const int B = c->sim_B;
+  if (B == 0) return KML_OK;
+  int slot = 0;
+  TRY(receive(c, c->s_y.as<double2>(), blind ? nullptr : c->s_h.as<double2>(), snr, B, nullptr, nullptr, nullptr,
+              nullptr, nullptr, c->s_uu.as<uint64_t>(), slot));
+  if (counters) {
+    unsigned long long h[kml::CNT_N];
+    HIPCHK(c, hipMemcpyAsync(h, slot_ptr(c, slot), sizeof(h), hipMemcpyDeviceToHost, c->stream), "D2H");
+    TRY(sync(c));
+    for (int i = 0; i < kml::CNT_N; i++) counters[i] = h[i];
+  }
+  return KML_OK;
+}
+
+int kml_sync(kml_ctx *c) {
+  if (!c) return KML_E_ARG;
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  return sync(c);
+}
+
+int kml_sim_frames(kml_ctx *c, uint8_t *uu, double *y, double *h) {
+  if (!c) return KML_E_ARG;
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const kml::LdpcCode &L = c->code;
+  const int B = c->sim_B, S = L.cc_len / c->modem.bits;
+  TRY(sync(c));
+  if (uu) {
+    std::vector<uint64_t> w((size_t)B * L.Kw);
+    HIPCHK(c, hipMemcpy(w.data(), c->s_uu.p, w.size() * 8, hipMemcpyDeviceToHost), "D2H");
+    for (int b = 0; b < B; b++)
+      for (int i = 0; i < L.K; i++) uu[(size_t)b * L.K + i] = (w[(size_t)b * L.Kw + (i >> 6)] >> (i & 63)) & 1;
+  }
+  if (y) HIPCHK(c, hipMemcpy(y, c->s_y.p, sizeof(double2) * (size_t)B * S, hipMemcpyDeviceToHost), "D2H");
+  if (h) HIPCHK(c, hipMemcpy(h, c->s_h.p, sizeof(double2) * (size_t)B, hipMemcpyDeviceToHost), "D2H");
+  return KML_OK;
+}
+
+int kml_prof_enable(kml_ctx *c, int on) {
+  if (!c) return KML_E_ARG;
+  c->prof = on != 0;
+  return KML_OK;
+}
+
+int kml_prof_reset(kml_ctx *c) {
+  if (!c) return KML_E_ARG;
+  drain_profile(c);
+  c->stats.clear();
+  return KML_OK;
+}
+
+int kml_prof_read(kml_ctx *c, const char *stage, int64_t *launches, double *total_ms, double *alg_bytes) {
+  if (!c || !stage) return KML_E_ARG;
+  if (c->device >= 0) hipSetDevice(c->device);
+  drain_profile(c);
+  Stat s;
+  auto it = c->stats.find(stage);
+  if (it != c->stats.end()) s = it->second;
+  if (launches) *launches = s.launches;
+  if (total_ms) *total_ms = s.ms;
+  if (alg_bytes) *alg_bytes = s.bytes;
+  return KML_OK;
+}
+
+int kml_math_probe(kml_ctx *c, const double *in, int n, double *out) {
+  if (!c || !in || !out || n < 0) return KML_E_ARG;
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const double *d_in;
+  TRY(stage_in(c, c->w_y, in, (size_t)n * 4, 0, d_in));
+  HIPCHK(c, c->w_p0.ensure(sizeof(double) * 4 * (size_t)n), "hipMalloc");
+  HIPCHK(c, kml::launch_math_probe(d_in, n, c->w_p0.as<double>(), c->stream), "probe");
+  TRY(copy_out(c, out, (const double *)c->w_p0.as<double>(), (size_t)n * 4, 0));
+  return sync(c);
+}
+
+}  // extern "C"

@@ -1,0 +1,245 @@
+// demap.hip — soft demapper, blind-candidate metric and error counting.
+//
+//   demap_kernel     ModemLinearSystem::SoftAWGNDemodulation
+//                    (lib/lab/src/modemlinearsystem.cc:51-79) followed by
+//                    Modem::DeMapping with bitLin = 0.5 (lib/lab/src/modem.cc:23-79;
+//                    KmCodec::DeMapping sets bit_l_in_ = 0.5, src/kmcodec.cc:96-98).
+//                    One thread per (codeword, symbol); the K-point loops run in
+//                    ascending k like the reference's sequential sums.
+//   cand_metric      KmCodec::GetMetrics + Metric with metric_type = false on a
+//                    PEG code (src/kmcodec.cc:122-142, :105-119): per codeword and
+//                    rotated estimate, count unsatisfied checks of rr = (P0 > 0.5);
+//                    argmin with first-minimum tie break (:59-65).  One workgroup
+//                    per codeword; hard decisions staged in LDS.
+//   select_kernel    the same argmin for the BP-based metrics (5G, :157-160).
+//   count_bytes      SourceSink::CntErr (lib/lab/src/sourcesink.cc:29-47).
+//
+// Numerics: every operation is the reference's IEEE operation in the
+// reference's order, except exp(), which is the ROCm device libm (ocml) rather
+// than glibc; both are within an ulp, so P0 can differ from the CPU path in the
+// last bit on a small fraction of symbols (measured and reported by the tests).
+#include "kernels.hpp"
+
+namespace kml {
+
+namespace {
+
+constexpr double kSmallestProb = 1.0e-12;
+
+__device__ __forceinline__ double prob_clip(double v) {  // utility.cc:18-26
+  if (v < kSmallestProb) return kSmallestProb;
+  if (v > 1.0 - kSmallestProb) return 1.0 - kSmallestProb;
+  return v;
+}
+
+// P0 for the MB bits of one symbol.
+template <int MB>
+__device__ __forceinline__ void demap_symbol(const double *__restrict__ cons, double yr, double yi, double hr, double hi,
+                                             double var, double *out) {
+  constexpr int KC = 1 << MB;
+  double pr[KC];
+  double mx = 0.0;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const double cr = cons[2 * k], ci = cons[2 * k + 1];
+    double sr = cr * hr - ci * hi;  // symbol *= theta_h
+    double si = cr * hi + ci * hr;
+    sr = sr - yr;  // symbol -= yy
+    si = si - yi;
+    const double d = (sr * sr + si * si) / var;
+    pr[k] = -d;
+    if (k == 0 || mx < pr[k]) mx = pr[k];  // *max_element
+  }
+  double sum = 0.0;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    pr[k] = exp(pr[k] - mx);
+    sum += pr[k];
+  }
+  // normalise + ProbClip (modemlinearsystem.cc:240-246), ProbClip again (modem.cc:27)
+  double w = 1.0;  // prod over bits of bitLin (= 0.5) or 1 - bitLin (= 0.5)
+#pragma unroll
+  for (int j = 0; j < MB; ++j) w *= 0.5;
+  double sum2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    pr[k] = prob_clip(prob_clip(pr[k] / sum));
+    pr[k] = w * pr[k];
+    sum2 += pr[k];
+  }
+#pragma unroll
+  for (int k = 0; k < KC; ++k) pr[k] /= sum2;
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    double q0 = 0.0, q1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      if (((k >> (MB - 1 - j)) & 1) == 0)
+        q0 += pr[k];
+      else
+        q1 += pr[k];
+    }
+    q0 /= 0.5;
+    q1 /= (1.0 - 0.5);
+    out[j] = prob_clip(q0 / (q0 + q1));
+  }
+}
+
+template <int MB>
+__global__ __launch_bounds__(256) void demap_kernel(const double *__restrict__ cons, const double2 *__restrict__ y,
+                                                    int S, int reps, const double2 *__restrict__ h, int h_stride,
+                                                    const int32_t *__restrict__ h_sel, double var, int B,
+                                                    double *__restrict__ p0) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long long)B * S) return;
+  const int ent = (int)(gid / S);
+  const int j = (int)(gid - (long long)ent * S);
+  const double2 hh = h[(long long)ent * h_stride + (h_sel ? h_sel[ent] : 0)];
+  const double2 yy = y[(long long)(ent / reps) * S + j];
+  double out[MB];
+  demap_symbol<MB>(cons, yy.x, yy.y, hh.x, hh.y, var, out);
+#pragma unroll
+  for (int j = 0; j < MB; ++j) p0[gid * MB + j] = out[j];
+}
+
+// One workgroup per codeword: hard decisions of the 4 candidates into LDS,
+// then the unsatisfied-check counts.
+template <int MB>
+__global__ __launch_bounds__(256) void cand_metric_kernel(DevCode c, const double *__restrict__ cons,
+                                                          const double2 *__restrict__ y, int S,
+                                                          const double2 *__restrict__ h4, double var,
+                                                          double *__restrict__ metrics, int32_t *__restrict__ chosen) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int *cnt = reinterpret_cast<int *>(smem);  // 4 counters
+  unsigned char *hb = smem + 16;             // [4][cc_len]
+  const int cw = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (tid < 4) cnt[tid] = 0;
+  const double2 *yy = y + (long long)cw * S;
+  for (int j = tid; j < S; j += blockDim.x) {
+    const double2 v = yy[j];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const double2 hh = h4[(long long)cw * 4 + q];
+      double out[MB];
+      demap_symbol<MB>(cons, v.x, v.y, hh.x, hh.y, var, out);
+#pragma unroll
+      for (int b = 0; b < MB; ++b) hb[q * c.cc_len + j * MB + b] = out[b] > 0.5 ? 1 : 0;  // kmcodec.cc:111-115
+    }
+  }
+  __syncthreads();
+  int local[4] = {0, 0, 0, 0};
+  for (int r = tid; r < c.M; r += blockDim.x) {
+    int p[4] = {0, 0, 0, 0};
+    for (int e = c.row_ptr[r]; e < c.row_ptr[r + 1]; ++e) {
+      const int col = c.row_col[e];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) p[q] ^= hb[q * c.cc_len + col];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) local[q] += p[q];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (local[q]) atomicAdd(&cnt[q], local[q]);
+  __syncthreads();
+  if (tid == 0) {
+    int best = 0;
+    for (int q = 0; q < 4; ++q) {
+      metrics[(long long)cw * 4 + q] = fabs((double)cnt[q]);
+      if (cnt[q] < cnt[best]) best = q;
+    }
+    chosen[cw] = best;
+  }
+}
+
+__global__ void select_kernel(const int32_t *__restrict__ pc, int B, double *__restrict__ metrics,
+                              int32_t *__restrict__ chosen) {
+  const int cw = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cw >= B) return;
+  int best = 0;
+  for (int q = 0; q < 4; ++q) {
+    metrics[(long long)cw * 4 + q] = fabs((double)pc[(long long)cw * 4 + q]);
+    if (pc[(long long)cw * 4 + q] < pc[(long long)cw * 4 + best]) best = q;
+  }
+  chosen[cw] = best;
+}
+
+__global__ void count_bytes_kernel(const uint8_t *__restrict__ uu, const uint8_t *__restrict__ uh, int K, int B,
+                                   unsigned long long *counters) {
+  // one workgroup per codeword
+  __shared__ int errs;
+  const int cw = blockIdx.x;
+  if (threadIdx.x == 0) errs = 0;
+  __syncthreads();
+  int e = 0;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) e += (uu[(long long)cw * K + i] != uh[(long long)cw * K + i]);
+  if (e) atomicAdd(&errs, e);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(&counters[CNT_ERR_BIT], (unsigned long long)errs);
+    atomicAdd(&counters[CNT_ERR_BLK], errs > 0 ? 1ull : 0ull);
+    atomicAdd(&counters[CNT_TOT_BIT], (unsigned long long)K);
+    atomicAdd(&counters[CNT_TOT_BLK], 1ull);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_demap(int bits, const double *cons, const double2 *y, int S, int reps, const double2 *h,
+                        int h_stride, const int32_t *h_sel, double var, int B, double *p0, hipStream_t s) {
+  const long long n = (long long)B * S;
+  if (n == 0) return hipSuccess;
+  const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
+  switch (bits) {
+    case 1: hipLaunchKernelGGL(demap_kernel<1>, grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0); break;
+    case 2: hipLaunchKernelGGL(demap_kernel<2>, grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0); break;
+    case 3: hipLaunchKernelGGL(demap_kernel<3>, grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0); break;
+    case 4: hipLaunchKernelGGL(demap_kernel<4>, grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0); break;
+    case 6: hipLaunchKernelGGL(demap_kernel<6>, grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, const double2 *y, int S,
+                              const double2 *h4, double var, int B, uint64_t * /*hard_ws*/, double *metrics,
+                              int32_t *chosen, hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  const size_t lds = 16 + 4 * (size_t)c.cc_len;
+  const dim3 grid(B), blk(256);
+  switch (bits) {
+#define KML_CM(MBV)                                                                                          \
+  case MBV: {                                                                                                \
+    hipError_t e = hipFuncSetAttribute((const void *)cand_metric_kernel<MBV>,                                \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
+    if (e != hipSuccess) return e;                                                                           \
+    hipLaunchKernelGGL(cand_metric_kernel<MBV>, grid, blk, lds, s, c, cons, y, S, h4, var, metrics, chosen); \
+    break;                                                                                                   \
+  }
+    KML_CM(1)
+    KML_CM(2)
+    KML_CM(3)
+    KML_CM(4)
+    KML_CM(6)
+#undef KML_CM
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_select(const int32_t *parity_cnt, int B, double *metrics, int32_t *chosen, hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  hipLaunchKernelGGL(select_kernel, dim3((B + 255) / 256), dim3(256), 0, s, parity_cnt, B, metrics, chosen);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_bytes(const uint8_t *uu, const uint8_t *uu_hat, int K, int B, unsigned long long *counters,
+                              hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  hipLaunchKernelGGL(count_bytes_kernel, dim3(B), dim3(256), 0, s, uu, uu_hat, K, B, counters);
+  return hipGetLastError();
+}
+
+}  // namespace kml

@@ -1,0 +1,102 @@
+// kernels.hpp — launch interfaces of the gfx950 kernels (host-visible).
+//
+// Layouts in HBM (B = codewords in the batch, codeword index slowest):
+//   y       [B][S] double2      received symbols
+//   h       [B] double2         per-codeword channel (true or estimated)
+//   p0      [B][cc_len] double  P(bit = 0) from the demapper (decoder input)
+//   uu_bits [B][Kw] u64         reference info bits, little-endian bit order
+//   cc_bits [B][Cw] u64         transmitted codeword bits
+//   uu_hat  [B][K] u8           decoded info bits (optional)
+// Decoder message state never leaves the chip for N <= ~9k edges: it lives in
+// LDS as one 16-byte slot per edge (see bp.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace kml {
+
+// Device-resident code description (uploaded once per context).
+struct DevCode {
+  const int32_t *row_ptr, *row_col, *col_ptr, *col_slot, *vn_order, *cn_order;
+  const uint64_t *enc_info;
+  int M, N, E, K, cc_len, punct, info_off, chk, Kw, dv_max, dc_max, is5g, active;
+};
+
+// Counter block in device memory (uint64):
+enum {
+  CNT_ERR_BIT = 0,
+  CNT_ERR_BLK = 1,
+  CNT_TOT_BIT = 2,
+  CNT_TOT_BLK = 3,
+  CNT_VN_PHASES = 4,
+  CNT_CN_PHASES = 5,
+  CNT_CONVERGED = 6,
+  CNT_N = 8
+};
+
+struct BpLaunch {
+  int B = 0;
+  int iter_count = 0, max_iter = 0;
+  const double *p0 = nullptr;
+  long long p0_stride = 0;       // doubles between codewords
+  const int32_t *p0_sel = nullptr;  // optional per-codeword candidate: p0 += sel*p0_sel_stride
+  long long p0_sel_stride = 0;
+  uint8_t *uu_hat = nullptr;     // [B][K]
+  int32_t *ret = nullptr;        // [B]  BinaryLDPCCodec::Decoder return value
+  uint8_t *cc_hat = nullptr;     // [B][N]
+  double *syn = nullptr;         // [B][M] syndrom_soft (written by CN phases only)
+  int32_t *parity_cnt = nullptr; // [B] unsatisfied checks of the final cc_hat
+  const uint64_t *ref_bits = nullptr;  // [B][Kw] for error counting
+  unsigned long long *counters = nullptr;  // [CNT_N]
+  double2 *gslots = nullptr;     // global slot scratch when E*16 exceeds LDS
+  long long gslots_cap = 0;      // number of double2 available
+  unsigned int *queue = nullptr; // 4-byte device dequeue counter (zeroed by the launcher)
+};
+
+// Returns hipSuccess or an error; `err` is set for configuration problems.
+hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const char **err);
+// Workspace the BP launcher needs in global-slot mode (double2 elements).
+long long bp_gslots_needed(const DevCode &c);
+bool bp_uses_lds(const DevCode &c);
+
+// SoftAWGNDemodulation + Modem::DeMapping with bitLin = 0.5, for `n` entries:
+// entry e reads y row e / reps and channel h[e * h_stride + (h_sel ? h_sel[e] : 0)],
+// writes p0 row e.  (reps = 4, h_stride = 1 demaps the 4 blind candidates.)
+hipError_t launch_demap(int bits, const double *cons, const double2 *y, int S, int reps, const double2 *h,
+                        int h_stride, const int32_t *h_sel, double var, int n, double *p0, hipStream_t s);
+
+// Hard-metric candidates for the PEG blind path (kmcodec.cc:105-119):
+// for each codeword and each of the 4 rotated estimates h4[b][j], the number of
+// unsatisfied checks of rr = (P0 > 0.5).  metrics[b][4] doubles, chosen[b].
+hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, const double2 *y, int S,
+                              const double2 *h4, double var, int B, uint64_t *hard_ws, double *metrics,
+                              int32_t *chosen, hipStream_t s);
+// argmin over a [B][4] metric table (first minimum) for the BP-based metrics.
+hipError_t launch_select(const int32_t *parity_cnt, int B, double *metrics, int32_t *chosen, hipStream_t s);
+
+// KMeans::Run + h_hat = clusters[0]/c[0] + 4 rotations, one lane per codeword.
+hipError_t launch_kmeans(int Kc, const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
+                         double2 *h_hat, double2 *h4, hipStream_t s);
+
+// GPU frame generation (counter-based Philox; statistically equivalent to the
+// reference's sequential Park-Miller stream, not bit-equal).
+struct FrameLaunch {
+  int B = 0;
+  unsigned long long seed = 0, first_cw = 0;
+  double noise_scale = 0;
+  uint64_t *uu_bits = nullptr;  // [B][Kw]
+  uint64_t *cc_bits = nullptr;  // [B][Cw]
+  double2 *y = nullptr;         // [B][S]
+  double2 *h = nullptr;         // [B]
+};
+hipError_t launch_framegen(const DevCode &c, int bits, const double *cons, const FrameLaunch &f, hipStream_t s);
+
+// Count mismatching bits: uu_hat bytes vs reference bits (SourceSink::CntErr).
+hipError_t launch_count_bytes(const uint8_t *uu, const uint8_t *uu_hat, int K, int B, unsigned long long *counters,
+                              hipStream_t s);
+
+// Device-side self tests of the exact-math helpers (hypot, complex division).
+hipError_t launch_math_probe(const double *in, int n, double *out, hipStream_t s);
+
+}  // namespace kml

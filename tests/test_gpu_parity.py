@@ -1,0 +1,292 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and
+the reference-generated golden fixtures.  Run on an MI355X with -m gpu.
+
+Bars:
+  * BP decoder (pure IEEE + - * /): bit-exact — uu_hat, return value, cc_hat
+    and syndrom_soft (which depends on every CN-phase message).
+  * k-means (hypot, Smith division, complex products): bit-exact h_hat.
+  * demapper: exp() is the device libm, so P0 may differ from glibc's in the
+    last bits; the test bounds that to 4 ulp (relative 1e-15) and requires the
+    hard decisions P0 > 0.5 to be identical.
+  * full KmCodec::Decoder path vs the reference stream fixtures: chosen
+    candidate, BP return value and uu_hat CRC; mismatches (from the exp ulp
+    differences) are counted and must be zero on the committed fixtures.
+"""
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, case_names, load_case
+from oracle import oracle as O
+
+import kmldpc_amd as K
+
+pytestmark = pytest.mark.gpu
+
+CASES = case_names()
+_ctx = {}
+
+
+def crc(a):
+    return zlib.crc32(np.ascontiguousarray(a).tobytes()) & 0xFFFFFFFF
+
+
+def ctx_for(data_dir, matrix, modem, is5g, max_iter=20, active=True):
+    key = (matrix, modem, is5g, max_iter, active)
+    if key not in _ctx:
+        _ctx[key] = K.Context(matrix_file=os.path.join(data_dir, matrix), modem_file=os.path.join(data_dir, modem),
+                              is5g=is5g, active=active, max_iter=max_iter, device=0)
+    return _ctx[key]
+
+
+_oc = {}
+
+
+def oracle_for(data_dir, matrix, is5g, max_iter=20, active=True):
+    key = (matrix, is5g, max_iter, active)
+    if key not in _oc:
+        _oc[key] = O.Code(os.path.join(data_dir, matrix), is5g, active, False, max_iter)
+    return _oc[key]
+
+
+def ulp_diff(a, b):
+    ia = a.view(np.int64)
+    ib = b.view(np.int64)
+    return np.abs(ia - ib)
+
+
+def test_device_exact_math_matches_host(data_dir):
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    rng = np.random.default_rng(1)
+    n = 400000
+    x = np.empty((n, 4))
+    s = 2.0 ** rng.uniform(-20, 20, n)
+    x[:, 0] = rng.normal(size=n) * s
+    x[:, 1] = rng.normal(size=n) * np.where(np.arange(n) % 3 == 0, s, 1.0)
+    x[:, 2] = rng.normal(size=n)
+    x[:, 3] = rng.normal(size=n) * (np.arange(n) % 5 != 0)
+    x[::17, 2] = np.arange(n)[::17] % 300 + 1.0
+    x[::17, 3] = 0.0
+    out = ctx.math_probe(x)
+    h_ref = np.array([O.lib().orc_hypot(a, b) for a, b in x[:, :2]])
+    assert np.array_equal(out[:, 0], h_ref)
+    q = np.array([O.cdiv(*r) for r in x[:20000]])
+    assert np.array_equal(out[:20000, 1:3], q)
+
+
+def test_device_exp_vs_glibc(data_dir):
+    """Report how often the device exp differs from glibc (used by the demapper)."""
+    import math
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    rng = np.random.default_rng(2)
+    n = 200000
+    x = np.zeros((n, 4))
+    x[:, 0] = -rng.exponential(8.0, n)
+    x[:, 2] = 1.0
+    out = ctx.math_probe(x)[:, 3]
+    ref = np.array([math.exp(v) for v in x[:, 0]])
+    d = ulp_diff(out, ref)
+    frac = float(np.mean(d != 0))
+    print(f"device exp != glibc exp on {frac:.2e} of inputs, max {int(d.max())} ulp")
+    assert d.max() <= 2
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_bp_golden_vectors(case, data_dir):
+    """Decode the reference's own P0 vectors: every output bit-exact."""
+    hdr, z = load_case(case)
+    ctx = ctx_for(data_dir, hdr["matrix"], hdr["modem"], bool(hdr["is5g"]), hdr["max_iter"])
+    p0 = z["v_p0"]
+    B = p0.shape[0]
+    syn0 = np.full((B, ctx.M), -1.0)
+    r = ctx.bp_decode(p0, cc_hat=True, syn=syn0)
+    assert np.array_equal(r["ret"], z["s_ret"][:B])
+    assert np.array_equal(r["uu_hat"], z["v_uu_hat"])
+    assert np.array_equal(r["cc_hat"], z["v_cc_hat"])
+    for i in range(B):
+        if r["ret"][i] > 1:
+            assert np.array_equal(r["syn"][i], z["v_syn"][i]), f"syndrom_soft cw {i}"
+
+
+@pytest.mark.parametrize("matrix,modem,is5g,snr,max_iter,n", [
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, 2.0, 20, 300),
+    ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", False, 4.0, 20, 200),
+    ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, 5.01, 50, 200),
+    ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 8.5, 20, 48),
+])
+def test_bp_vs_oracle_stream(data_dir, matrix, modem, is5g, snr, max_iter, n):
+    """Oracle frames -> oracle P0 -> GPU BP vs oracle BP, bit-exact incl. the
+    syndrome messages, plus a short iteration budget (the metric BP)."""
+    ctx = ctx_for(data_dir, matrix, modem, is5g, max_iter)
+    oc = oracle_for(data_dir, matrix, is5g, max_iter)
+    om = O.Modem(os.path.join(data_dir, modem))
+    uu, cc, th, y = O.gen_frames(oc, om, snr, n)
+    var = 10.0 ** (-0.1 * snr)
+    p0 = np.stack([om.demap(y[i], th[i], var) for i in range(n)])
+    for it in (max_iter, 5, 1):
+        r = ctx.bp_decode(p0, iter_count=it, cc_hat=True, syn=np.zeros((n, ctx.M)))
+        for i in range(n):
+            ret, uh, cch, syn = oc.bp_decode(p0[i], it)
+            assert r["ret"][i] == ret, (it, i)
+            assert np.array_equal(r["uu_hat"][i], uh), (it, i)
+            assert np.array_equal(r["cc_hat"][i], cch), (it, i)
+            assert np.array_equal(r["syn"][i], syn), (it, i)
+
+
+@pytest.mark.parametrize("matrix,modem,is5g,snr,n", [
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, 2.0, 200),
+    ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", False, 5.0, 100),
+    ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 6.77, 40),
+])
+def test_demap_vs_oracle(data_dir, matrix, modem, is5g, snr, n):
+    ctx = ctx_for(data_dir, matrix, modem, is5g)
+    oc = oracle_for(data_dir, matrix, is5g)
+    om = O.Modem(os.path.join(data_dir, modem))
+    uu, cc, th, y = O.gen_frames(oc, om, snr, n)
+    var = 10.0 ** (-0.1 * snr)
+    ref = np.stack([om.demap(y[i], th[i], var) for i in range(n)])
+    got = ctx.demap(y, th, var)
+    d = ulp_diff(got.reshape(-1), ref.reshape(-1))
+    print(f"demap: {np.mean(d != 0):.2e} of P0 differ, max {int(d.max())} ulp")
+    assert np.array_equal(got > 0.5, ref > 0.5)
+    assert np.all(np.abs(got - ref) <= 1e-15 * np.abs(ref) + 1e-300)
+
+
+@pytest.mark.parametrize("matrix,modem,snr,n", [
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", 2.0, 200),
+    ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", 5.01, 100),
+    ("PEG2304regular0.5.txt", "4bit_16QAM_phi1.txt", 8.0, 50),
+    ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", 6.77, 30),
+])
+def test_kmeans_vs_oracle(data_dir, matrix, modem, snr, n):
+    ctx = ctx_for(data_dir, matrix, modem, False)
+    oc = oracle_for(data_dir, matrix, False)
+    om = O.Modem(os.path.join(data_dir, modem))
+    uu, cc, th, y = O.gen_frames(oc, om, snr, n)
+    hh, h4 = ctx.kmeans(y)
+    for i in range(n):
+        ref = O.kmeans_hhat(y[i], om.points)
+        assert np.array_equal(hh[i], ref), i
+        assert np.array_equal(h4[i], O.rotations(ref)), i
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_decode_frames_vs_reference_stream(case, data_dir):
+    """KmCodec::Decoder on the reference's own frames (regenerated bit-exactly
+    by the oracle, pinned by the y CRCs): chosen candidate, BP return value,
+    decoded bits and error counts equal the reference's."""
+    hdr, z = load_case(case)
+    ctx = ctx_for(data_dir, hdr["matrix"], hdr["modem"], bool(hdr["is5g"]), hdr["max_iter"])
+    oc = oracle_for(data_dir, hdr["matrix"], bool(hdr["is5g"]), hdr["max_iter"])
+    om = O.Modem(os.path.join(data_dir, hdr["modem"]))
+    n = hdr["ncw"]
+    uu, cc, th, y = O.gen_frames(oc, om, hdr["snr"], n)
+    assert all(crc(y[i]) == z["s_crc_y"][i] for i in range(n))
+    r = ctx.decode_frames(y, hdr["snr"], None if not hdr["known"] else th)
+    bad = [i for i in range(n) if crc(r["uu_hat"][i]) != z["s_crc_uuhat"][i]]
+    assert not bad, f"{len(bad)}/{n} codewords differ: {bad[:10]}"
+    assert np.array_equal(r["ret"], z["s_ret"][:n])
+    if not hdr["known"]:
+        assert np.array_equal(r["chosen"], z["s_chosen"][:n])
+        assert np.array_equal(r["metrics"], z["s_metrics"][:n])
+        assert np.array_equal(r["h_hat"], z["s_hhat"][:n])
+    cnt = ctx.count_errors(uu.astype(np.uint8), r["uu_hat"])
+    assert cnt["err_bit"] == int(z["s_errs"][:n].sum())
+    assert cnt["err_blk"] == int((z["s_errs"][:n] > 0).sum())
+    assert cnt["tot_blk"] == n
+
+
+def test_reference_counters_2000(data_dir):
+    """End-to-end SourceSink counters of the reference (2000 cw, seed 17)."""
+    ctr = json.load(open(os.path.join(GOLDEN, "counters.json")))
+    for name, c in ctr.items():
+        ctx = ctx_for(data_dir, c["matrix"], c["modem"], c["is5g"], c["max_iter"])
+        oc = oracle_for(data_dir, c["matrix"], c["is5g"], c["max_iter"])
+        om = O.Modem(os.path.join(data_dir, c["modem"]))
+        uu, cc, th, y = O.gen_frames(oc, om, c["snr"], c["n"])
+        r = ctx.decode_frames(y, c["snr"], th if c["known"] else None)
+        cnt = ctx.count_errors(uu.astype(np.uint8), r["uu_hat"])
+        assert (cnt["err_blk"], cnt["err_bit"], cnt["tot_blk"]) == (c["err_blk"], c["err_bit"], c["tot_blk"]), name
+
+
+def test_gpu_frames_are_codewords_and_channel_consistent(data_dir):
+    """GPU frame generation: at very high SNR the known-H path decodes every
+    codeword without error at iteration 0, and the frames are reproducible."""
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    ctx.sim_generate(60.0, 256, seed=3, first_cw=1000)
+    c = ctx.sim_decode(60.0, blind=False)
+    assert c["tot_blk"] == 256 and c["err_blk"] == 0 and c["converged"] == 256 and c["cn_phases"] == 0
+    uu1, y1, h1 = ctx.sim_frames(256)
+    ctx.sim_generate(60.0, 128, seed=3, first_cw=1128)  # a sub-range regenerates identical frames
+    uu2, y2, h2 = ctx.sim_frames(128)
+    assert np.array_equal(uu1[128:], uu2) and np.array_equal(y1[128:], y2) and np.array_equal(h1[128:], h2)
+    # transmitted bits are codewords: hard-decode y/h at 60 dB and check
+    x = (y1[:, :, 0] + 1j * y1[:, :, 1]) / (h1[:, 0] + 1j * h1[:, 1])[:, None]
+    assert abs(np.mean(np.abs(x) ** 2) - 1.0) < 1e-3
+
+
+def test_gpu_monte_carlo_matches_reference_statistics(data_dir):
+    """BER/FER of GPU-generated frames at the BASELINE point (PEG2304 QPSK,
+    Es/N0 2 dB, known H, 20 it) agree with the reference's seed-17 counters
+    (2000 cw: FER 0.586, BER 0.13467) within Monte-Carlo confidence."""
+    ctr = json.load(open(os.path.join(GOLDEN, "counters.json")))["peg2304_qpsk_known_2000"]
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    B = 20000
+    ctx.sim_generate(2.0, B, seed=11)
+    c = ctx.sim_decode(2.0, blind=False)
+    fer = c["err_blk"] / c["tot_blk"]
+    ref = ctr["fer"]
+    sigma = np.sqrt(ref * (1 - ref) / ctr["n"] + ref * (1 - ref) / B)
+    print(f"GPU FER {fer:.4f} vs reference {ref:.4f} (sigma {sigma:.4f})")
+    assert abs(fer - ref) < 4 * sigma
+    ber = c["err_bit"] / c["tot_bit"]
+    assert abs(ber - ctr["ber"]) < 0.02
+
+
+def test_blind_gpu_monte_carlo(data_dir):
+    ctr = json.load(open(os.path.join(GOLDEN, "counters.json")))["peg2304_qpsk_blind_2000"]
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    B = 8000
+    ctx.sim_generate(2.0, B, seed=12)
+    c = ctx.sim_decode(2.0, blind=True)
+    fer = c["err_blk"] / c["tot_blk"]
+    ref = ctr["fer"]
+    sigma = np.sqrt(ref * (1 - ref) / ctr["n"] + ref * (1 - ref) / B)
+    print(f"GPU blind FER {fer:.4f} vs reference {ref:.4f} (sigma {sigma:.4f})")
+    assert abs(fer - ref) < 4 * sigma
+
+
+def test_empty_and_ragged_batches(data_dir):
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    r = ctx.bp_decode(np.zeros((0, ctx.cc_len)))
+    assert r["uu_hat"].shape == (0, ctx.K)
+    # odd batch sizes around the grid size
+    rng = np.random.default_rng(9)
+    for B in (1, 3, 257, 513):
+        p0 = rng.uniform(0.05, 0.95, (B, ctx.cc_len))
+        r = ctx.bp_decode(p0, iter_count=3)
+        oc = oracle_for(data_dir, "PEG2304regular0.5.txt", False)
+        for i in (0, B - 1):
+            ret, uh, _, _ = oc.bp_decode(p0[i], 3)
+            assert r["ret"][i] == ret and np.array_equal(r["uu_hat"][i], uh)
+
+
+def test_extreme_inputs_match_oracle(data_dir):
+    """Saturated / tie / NaN-free edge inputs: P0 at the clip bounds, exactly
+    0.5 everywhere (every hard decision is a tie -> 1), and 0/1 extremes."""
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    oc = oracle_for(data_dir, "PEG2304regular0.5.txt", False)
+    n = ctx.cc_len
+    rng = np.random.default_rng(4)
+    cases = [np.full(n, 0.5), np.full(n, 1e-12), np.full(n, 1 - 1e-12),
+             np.where(rng.random(n) < 0.5, 1e-12, 1 - 1e-12), rng.choice([0.0, 1.0, 0.5], n)]
+    p0 = np.stack(cases)
+    r = ctx.bp_decode(p0, cc_hat=True, syn=np.zeros((len(cases), ctx.M)))
+    for i in range(len(cases)):
+        ret, uh, cch, syn = oc.bp_decode(p0[i])
+        assert r["ret"][i] == ret
+        assert np.array_equal(r["cc_hat"][i], cch)
+        assert np.array_equal(r["syn"][i], syn, equal_nan=True)

@@ -1,0 +1,163 @@
+"""CPU-side tests of the product library (no GPU): the C ABI loads and exports
+every symbol include/kmldpc_amd.h declares, the host planner (config parsing,
+H-matrix parsing, GF(2) elimination, graph order, encoder, constellation) is
+bit-identical to the oracle, and the exact-math restatements used by the
+device code equal glibc / libgcc on the host."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO, load_case, write_config
+from oracle import oracle as O
+
+import kmldpc_amd as K
+
+CODES = [
+    ("PEG2304regular0.5.txt", False),
+    ("5GLDPCBG2a3_R12_K960.txt", True),
+    ("PEG8064regular0.5.txt", False),
+]
+MODEMS = ["2bits_QPSK.txt", "2bits_4PSK.txt", "4bit_16QAM_Gray.txt", "4bit_16QAM_phi1.txt", "4bit_16QAM_phi2.txt",
+          "6bits_64QAM_Gray.txt"]
+
+
+def test_library_exports_header_symbols():
+    L = K.lib()
+    syms = K.header_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert L.kml_abi_version() == 1
+
+
+_oracle_codes = {}
+
+
+def oracle_code(data_dir, matrix, is5g, active=True):
+    key = (matrix, active)
+    if key not in _oracle_codes:
+        _oracle_codes[key] = O.Code(os.path.join(data_dir, matrix), is5g, active, False, 20)
+    return _oracle_codes[key]
+
+
+@pytest.mark.parametrize("matrix,is5g", CODES)
+@pytest.mark.parametrize("active", [True, False])
+def test_planner_matches_oracle(data_dir, matrix, is5g, active):
+    if "8064" in matrix and not active:
+        pytest.skip("covered by the active case")
+    ctx = K.Context(matrix_file=os.path.join(data_dir, matrix), modem_file=os.path.join(data_dir, "2bits_QPSK.txt"),
+                    is5g=is5g, active=active, device=-1)
+    oc = oracle_code(data_dir, matrix, is5g, active)
+    assert (ctx.M, ctx.Ncol, ctx.K, ctx.cc_len, ctx.Z, ctx.E, ctx.chk) == (oc.M, oc.N, oc.K, oc.cc_len, oc.Z, oc.E,
+                                                                           oc.chk)
+    assert np.array_equal(ctx.perm(), oc.perm())
+    for a, b in zip(ctx.graph(), oc.graph()):
+        assert np.array_equal(a, b)
+    rng = np.random.default_rng(5)
+    uu = rng.integers(0, 2, (6, ctx.K)).astype(np.uint8)
+    cc = ctx.encode(uu)
+    for i in range(uu.shape[0]):
+        assert np.array_equal(cc[i], oc.encode(uu[i].astype(np.int32)).astype(np.uint8))
+    if active:  # every codeword satisfies H (graph columns are the permuted ones)
+        for i in range(uu.shape[0]):
+            full = np.zeros(ctx.Ncol, np.uint8)
+            full[ctx.Ncol - ctx.cc_len:] = cc[i]
+            if is5g:  # punctured columns are the first 2Z info bits
+                full[:2 * ctx.Z] = uu[i][:2 * ctx.Z]
+            assert oc.parity_count(full) == 0
+
+
+@pytest.mark.parametrize("modem", MODEMS)
+def test_constellation_matches_oracle(data_dir, modem):
+    ctx = K.Context(matrix_file=os.path.join(data_dir, "PEG2304regular0.5.txt"),
+                    modem_file=os.path.join(data_dir, modem), device=-1)
+    om = O.Modem(os.path.join(data_dir, modem))
+    assert np.array_equal(ctx.constellation().reshape(-1), om.points)
+
+
+def test_constellation_matches_reference_fixture(data_dir):
+    hdr, z = load_case("peg8064_64qam_blind")
+    ctx = K.Context(matrix_file=os.path.join(data_dir, "PEG2304regular0.5.txt"),
+                    modem_file=os.path.join(data_dir, hdr["modem"]), device=-1)
+    assert np.array_equal(ctx.constellation(), z["cons"])
+
+
+def test_config_file_parsing(tmp_path, data_dir):
+    cfg = tmp_path / "config.toml"
+    write_config(str(cfg), data_dir, "5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", is5g=True, max_iter=50,
+                 metric_iter=7)
+    ctx = K.Context(str(cfg), device=-1)
+    assert ctx.K == 960 and ctx.cc_len == 1920 and ctx.Z == 96 and ctx.max_iter == 50 and ctx.bits == 4
+
+
+def test_config_relative_paths_resolve_against_data_dir(tmp_path, data_dir):
+    cfg = tmp_path / "config.toml"
+    cfg.write_text("""# range
+[range]
+    minimum_snr = 15.0
+    maximum_snr = 15.0
+    step_snr = 5.0
+    maximum_error_number = 1
+    maximum_block_number = 1
+    # maximum blocks for each threads under the snr
+    thread_block_number = 1
+
+[decoder]
+    true_h_arg = false
+
+[xcodec]
+    # default, using normal ldcp.
+    5gldpc = false
+    # (false) hard metric, (true) soft metric
+    metric_type = false
+    # only use for 5g ldpc
+    metric_iter = 5
+
+[histogram]
+    enable = false
+
+[ldpc]
+    max_iter = 50
+    # (false) not encode, (true) encode
+    active = true
+    matrix_file = "PEG2304regular0.5.txt"
+
+[modem]
+    modem_file = "4bit_16QAM_Gray.txt"
+""")
+    ctx = K.Context(str(cfg), data_dir=data_dir, device=-1)
+    assert ctx.K == 1152 and ctx.max_iter == 50 and ctx.Kc == 16
+
+
+def test_errors_are_reported_not_fatal(tmp_path, data_dir):
+    with pytest.raises(K.KmlError, match="Cannot open"):
+        K.Context(matrix_file=str(tmp_path / "missing.txt"), modem_file=os.path.join(data_dir, "2bits_QPSK.txt"),
+                  device=-1)
+    bad = tmp_path / "bad.toml"
+    bad.write_text("[ldpc]\nmax_iter = 20\n")
+    with pytest.raises(K.KmlError, match="missing"):
+        K.Context(str(bad), device=-1)
+    lab = tmp_path / "badmodem.txt"
+    lab.write_text("bits\n2\ndims\n2\nhdr\n0 0 0 1 0\n2 0 1 0 1\n")  # label mismatch (modem.cc:113-118)
+    with pytest.raises(K.KmlError, match="binary expression"):
+        K.Context(matrix_file=os.path.join(data_dir, "PEG2304regular0.5.txt"), modem_file=str(lab), device=-1)
+
+
+def test_host_only_context_refuses_gpu_calls(data_dir):
+    ctx = K.Context(matrix_file=os.path.join(data_dir, "PEG2304regular0.5.txt"),
+                    modem_file=os.path.join(data_dir, "2bits_QPSK.txt"), device=-1)
+    with pytest.raises(K.KmlError, match="host-only"):
+        ctx.bp_decode(np.full((1, ctx.cc_len), 0.9))
+
+
+def test_exact_math_host_restatement(tmp_path):
+    """kml_hypot / kml_cdiv (kmldpc_amd/csrc/exact_math.hpp) vs glibc hypot and
+    libgcc __divdc3 — the routines std::abs / operator/ call in the reference."""
+    exe = tmp_path / "emc"
+    src = os.path.join(REPO, "tests", "native", "exact_math_check.cpp")
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", "-o", str(exe), src], check=True)
+    out = subprocess.run([str(exe), "1000000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    assert "hypot_mismatch=0 cdiv_mismatch=0" in out.stdout
