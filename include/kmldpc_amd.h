@@ -148,7 +148,8 @@ int kml_prof_reset(kml_ctx *ctx);
 int kml_prof_read(kml_ctx *ctx, const char *stage, int64_t *launches, double *total_ms, double *alg_bytes);
 
 /* Device-side probe of the exact-math helpers: in[n][4] = (a, b, c, d) ->
- * out[n][4] = (hypot(a,b), re((a+ib)/(c+id)), im(...), exp(a)). */
+ * out[n][4] = (hypot(a,b), re((a+ib)/(c+id)), im(...), exp(a)) with the
+ * glibc-exact restatements the kernels use. */
 int kml_math_probe(kml_ctx *ctx, const double *in, int n, double *out);
 
 #ifdef __cplusplus

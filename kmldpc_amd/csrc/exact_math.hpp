@@ -16,6 +16,13 @@
 //                do not change the quotient for the finite, non-extreme values
 //                this path divides (cluster sums, received symbols,
 //                constellation points).
+//   kml_exp    — glibc >= 2.28 exp (sysdeps/ieee754/dbl-64/e_exp.c, the
+//                table-driven algorithm of ARM optimized-routines: N = 128,
+//                degree-5 polynomial), in the contraction pattern of the x86-64
+//                FMA ifunc variant (__exp_fma) that glibc selects on every
+//                FMA-capable host — the one the reference's demapper calls
+//                (lib/lab/src/modemlinearsystem.cc:61).  The 2^(k/128) table is
+//                regenerated from first principles (tools/gen_exp_table.py).
 //   kml_cmul   — std::complex<double> operator* as GCC expands it without
 //                -ffast-math: (ac - bd, ad + bc); the __muldc3 fallback is
 //                reached only when both parts are NaN.
@@ -34,6 +41,8 @@
 
 #include <cmath>
 #include <cstdint>
+
+#include "exp_table.hpp"
 
 namespace kml {
 
@@ -128,6 +137,87 @@ KML_HD cplx kml_cdiv(cplx n, cplx dd) {
   }
   return cplx{x, y};
 }
+
+KML_HD uint64_t as_u64(double x) { return __builtin_bit_cast(uint64_t, x); }
+KML_HD double as_f64(uint64_t x) { return __builtin_bit_cast(double, x); }
+
+KML_HD uint64_t exp_tab(int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return kExpTabDev[i];
+#else
+  return kExpTabHost[i];
+#endif
+}
+
+// FMA selects the contraction pattern of the FMA-compiled glibc variant.
+template <bool FMA>
+KML_HD double exp_special(double tmp, uint64_t sbits, uint64_t ki) {
+  double scale, y;
+  if ((ki & 0x80000000) == 0) {  // k > 0: the exponent of scale may have overflowed by <= 460
+    sbits -= 1009ull << 52;
+    scale = as_f64(sbits);
+    y = 0x1p1009 * (FMA ? fma(scale, tmp, scale) : scale + scale * tmp);
+    return y;
+  }
+  sbits += 1022ull << 52;  // k < 0: careful rounding into the subnormal range
+  scale = as_f64(sbits);
+  // scale*tmp has two uses here and is not fused in the FMA build
+  const double st = scale * tmp;
+  y = scale + st;
+  if (y < 1.0) {
+    double hi, lo;
+    lo = scale - y + st;
+    hi = 1.0 + y;
+    lo = 1.0 - hi + y + lo;
+    y = (hi + lo) - 1.0;
+    if (y == 0.0) y = 0.0;
+  }
+  return 0x1p-1022 * y;
+}
+
+template <bool FMA>
+KML_HD double kml_exp_t(double x) {
+  const double InvLn2N = 0x1.71547652b82fep0 * 128;
+  const double Shift = 0x1.8p52;
+  const double NegLn2hiN = -0x1.62e42fefa0000p-8;
+  const double NegLn2loN = -0x1.cf79abc9e3b3ap-47;
+  const double C2 = 0x1.ffffffffffdbdp-2, C3 = 0x1.555555555543cp-3;
+  const double C4 = 0x1.55555cf172b91p-5, C5 = 0x1.1111167a4d017p-7;
+  const uint32_t top_tiny = (uint32_t)(as_u64(0x1p-54) >> 52);
+  const uint32_t top_512 = (uint32_t)(as_u64(512.0) >> 52);
+  const uint32_t top_1024 = (uint32_t)(as_u64(1024.0) >> 52);
+  const uint32_t top_inf = (uint32_t)(as_u64(INFINITY) >> 52);
+  uint32_t abstop = (uint32_t)(as_u64(x) >> 52) & 0x7ff;
+  if (abstop - top_tiny >= top_512 - top_tiny) {
+    if (abstop - top_tiny >= 0x80000000u) return 1.0 + x;  // tiny |x| (incl. 0)
+    if (abstop >= top_1024) {
+      if (as_u64(x) == as_u64(-INFINITY)) return 0.0;
+      if (abstop >= top_inf) return 1.0 + x;
+      if (as_u64(x) >> 63) return 0x1p-767 * 0x1p-767;  // underflow
+      return 0x1p769 * 0x1p769;                          // overflow
+    }
+    abstop = 0;  // large |x|: special-cased below
+  }
+  double kd = FMA ? fma(InvLn2N, x, Shift) : InvLn2N * x + Shift;
+  const uint64_t ki = as_u64(kd);
+  kd -= Shift;
+  const double r = FMA ? fma(kd, NegLn2loN, fma(kd, NegLn2hiN, x)) : x + kd * NegLn2hiN + kd * NegLn2loN;
+  const int idx = (int)(2 * (ki % 128));
+  const uint64_t top = ki << (52 - 7);
+  const double tail = as_f64(exp_tab(idx));
+  const uint64_t sbits = exp_tab(idx + 1) + top;
+  const double r2 = r * r;
+  double tmp;
+  if (FMA)
+    tmp = fma(r2 * r2, fma(r, C5, C4), fma(r2, fma(r, C3, C2), tail + r));
+  else
+    tmp = tail + r + r2 * (C2 + r * C3) + r2 * r2 * (C4 + r * C5);
+  if (abstop == 0) return exp_special<FMA>(tmp, sbits, ki);
+  const double scale = as_f64(sbits);
+  return FMA ? fma(scale, tmp, scale) : scale + scale * tmp;
+}
+
+KML_HD double kml_exp(double x) { return kml_exp_t<true>(x); }
 
 KML_HD cplx kml_cmul(cplx a, cplx b) { return cplx{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
 

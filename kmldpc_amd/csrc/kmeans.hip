@@ -121,7 +121,7 @@ __global__ void math_probe_kernel(const double *in, int n, double *out) {
   const cplx q = kml_cdiv(cplx{a, b}, cplx{c, d});
   out[4 * i + 1] = q.re;
   out[4 * i + 2] = q.im;
-  out[4 * i + 3] = exp(a);
+  out[4 * i + 3] = kml_exp(a);
 }
 }  // namespace
 

@@ -5,12 +5,9 @@ Bars:
   * BP decoder (pure IEEE + - * /): bit-exact — uu_hat, return value, cc_hat
     and syndrom_soft (which depends on every CN-phase message).
   * k-means (hypot, Smith division, complex products): bit-exact h_hat.
-  * demapper: exp() is the device libm, so P0 may differ from glibc's in the
-    last bits; the test bounds that to 4 ulp (relative 1e-15) and requires the
-    hard decisions P0 > 0.5 to be identical.
+  * demapper (exp = kml_exp, the glibc-exact restatement): bit-exact P0.
   * full KmCodec::Decoder path vs the reference stream fixtures: chosen
-    candidate, BP return value and uu_hat CRC; mismatches (from the exp ulp
-    differences) are counted and must be zero on the committed fixtures.
+    candidate, metrics, h_hat, BP return value and uu_hat, bit-exact.
 """
 import json
 import os
@@ -78,7 +75,7 @@ def test_device_exact_math_matches_host(data_dir):
 
 
 def test_device_exp_vs_glibc(data_dir):
-    """Report how often the device exp differs from glibc (used by the demapper)."""
+    """The demapper's exp (kml_exp) equals glibc's exp bit for bit on device."""
     import math
     ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
     rng = np.random.default_rng(2)
@@ -88,10 +85,7 @@ def test_device_exp_vs_glibc(data_dir):
     x[:, 2] = 1.0
     out = ctx.math_probe(x)[:, 3]
     ref = np.array([math.exp(v) for v in x[:, 0]])
-    d = ulp_diff(out, ref)
-    frac = float(np.mean(d != 0))
-    print(f"device exp != glibc exp on {frac:.2e} of inputs, max {int(d.max())} ulp")
-    assert d.max() <= 2
+    assert np.array_equal(out, ref)
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -151,8 +145,7 @@ def test_demap_vs_oracle(data_dir, matrix, modem, is5g, snr, n):
     got = ctx.demap(y, th, var)
     d = ulp_diff(got.reshape(-1), ref.reshape(-1))
     print(f"demap: {np.mean(d != 0):.2e} of P0 differ, max {int(d.max())} ulp")
-    assert np.array_equal(got > 0.5, ref > 0.5)
-    assert np.all(np.abs(got - ref) <= 1e-15 * np.abs(ref) + 1e-300)
+    assert np.array_equal(got, ref)
 
 
 @pytest.mark.parametrize("matrix,modem,snr,n", [

@@ -161,3 +161,14 @@ def test_exact_math_host_restatement(tmp_path):
     out = subprocess.run([str(exe), "1000000"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
     assert "hypot_mismatch=0 cdiv_mismatch=0" in out.stdout
+
+
+def test_exp_host_restatement(tmp_path):
+    """kml_exp (glibc's table-driven exp, FMA-variant contraction pattern,
+    table regenerated by tools/gen_exp_table.py) equals the host glibc exp."""
+    exe = tmp_path / "expc"
+    src = os.path.join(REPO, "tests", "native", "exp_check.cpp")
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", "-o", str(exe), src], check=True)
+    out = subprocess.run([str(exe), "2000000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    assert "exp_fma_mismatch=0" in out.stdout
