@@ -151,6 +151,9 @@ int kml_prof_read(kml_ctx *ctx, const char *stage, int64_t *launches, double *to
  * out[n][4] = (hypot(a,b), re((a+ib)/(c+id)), im(...), exp(a)) with the
  * glibc-exact restatements the kernels use. */
 int kml_math_probe(kml_ctx *ctx, const double *in, int n, double *out);
+/* Device-side probe of the decoder's shared-reciprocal division: in[n][3] =
+ * (n0, n1, s) -> out[n][4] = (fast n0/s, fast n1/s, IEEE n0/s, IEEE n1/s). */
+int kml_div_probe(kml_ctx *ctx, const double *in, int n, double *out);
 
 #ifdef __cplusplus
 }

@@ -70,6 +70,7 @@ def lib():
         "kml_prof_reset": (I, [P]),
         "kml_prof_read": (I, [P, C.c_char_p, P, P, P]),
         "kml_math_probe": (I, [P, P, I, P]),
+        "kml_div_probe": (I, [P, P, I, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -262,6 +263,12 @@ class Context:
         by = np.zeros(1)
         self._chk(lib().kml_prof_read(self._h, stage.encode(), _p(n), _p(ms), _p(by)), "kml_prof_read")
         return dict(launches=int(n[0]), ms=float(ms[0]), bytes=float(by[0]))
+
+    def div_probe(self, x):
+        x = _f64(x).reshape(-1, 3)
+        out = np.zeros((x.shape[0], 4))
+        self._chk(lib().kml_div_probe(self._h, _p(x), x.shape[0], _p(out)), "kml_div_probe")
+        return out
 
     def math_probe(self, x):
         x = _f64(x).reshape(-1, 4)

@@ -27,13 +27,15 @@
 //
 // Compulsory-traffic accounting is accumulated in the counter
 // block: executed VN and CN phases per launch.
+#include <cstdlib>
+
+#include "bp_common.hpp"
 #include "kernels.hpp"
 
 namespace kml {
 
 namespace {
 
-constexpr double kSmallestProb = 1.0e-12;  // lib/lab/include/utility.h:12
 constexpr int kLdsBytes = 160 * 1024;
 constexpr int kRedBytes = 16;
 
@@ -287,6 +289,17 @@ hipError_t dispatch_deg(const DevCode &c, const BpLaunch &a, unsigned int *queue
 
 }  // namespace
 
+namespace {
+bool force_generic() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("KML_BP_GENERIC");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+}  // namespace
+
 bool bp_uses_lds(const DevCode &c) { return (long long)c.E * 16 + kRedBytes + c.N <= kLdsBytes; }
 
 long long bp_gslots_needed(const DevCode &c) {
@@ -309,6 +322,10 @@ hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const c
     return hipErrorInvalidValue;
   }
   const bool lds = bp_uses_lds(c);
+  if (lds && !force_generic()) {
+    hipError_t e = launch_bp_static(c, a, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   if (!lds && (a.gslots == nullptr || a.gslots_cap < c.E)) {
     if (err) *err = "global slot workspace missing";
     return hipErrorInvalidValue;

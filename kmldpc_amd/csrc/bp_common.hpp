@@ -1,0 +1,67 @@
+// bp_common.hpp — device helpers shared by the BP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace kml {
+
+constexpr double kSmallestProb = 1.0e-12;  // lib/lab/include/utility.h:12
+
+// q0 = n0 / s and q1 = n1 / s, both correctly rounded.
+//
+// FAST = false: two IEEE divisions.
+// FAST = true : one shared reciprocal refinement and two residual corrections —
+// exactly the instruction sequence hipcc emits for an f64 '/' on gfx950
+// (v_div_scale, v_rcp_f64, 2 Newton steps, v_mul, residual fma, v_div_fmas,
+// v_div_fixup) with the scale / fixup steps dropped.  Those steps are identity
+// operations unless an operand or the quotient is outside the normal range
+// (denominator or quotient denormal, numerator < 2^-969, exponent gap >= 768,
+// zero / inf / NaN denominators).  The caller guarantees that: it takes the FAST
+// path only for codewords whose priors are 0, 1 or in [2^-40, 1-2^-40] on codes
+// with column degree <= 20, which bounds every nonzero message, sum and quotient
+// of the decoder below 1 and above 2^-840 ("Exact fast division").
+template <bool FAST>
+__device__ __forceinline__ void div2(double n0, double n1, double s, double &q0, double &q1) {
+  if constexpr (!FAST) {
+    q0 = n0 / s;
+    q1 = n1 / s;
+  } else {
+    const double ns = -s;
+    double r = __builtin_amdgcn_rcp(s);
+    double e = fma(ns, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(ns, r, 1.0);
+    r = fma(r, e, r);
+    const double m0 = n0 * r;
+    const double m1 = n1 * r;
+    const double f0 = fma(ns, m0, n0);
+    const double f1 = fma(ns, m1, n1);
+    q0 = fma(f0, r, m0);
+    q1 = fma(f1, r, m1);
+  }
+}
+
+template <bool FAST>
+__device__ __forceinline__ double div1(double n0, double s) {
+  if constexpr (!FAST) {
+    return n0 / s;
+  } else {
+    const double ns = -s;
+    double r = __builtin_amdgcn_rcp(s);
+    double e = fma(ns, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(ns, r, 1.0);
+    r = fma(r, e, r);
+    const double m0 = n0 * r;
+    const double f0 = fma(ns, m0, n0);
+    return fma(f0, r, m0);
+  }
+}
+
+// Prior values for which the FAST division path is exact (see div2).
+__device__ __forceinline__ bool fast_prior_ok(double q) {
+  return q == 0.0 || q == 1.0 || (q >= 0x1p-40 && q <= 1.0 - 0x1p-40);
+}
+
+constexpr int kFastMaxColumnDegree = 20;
+
+}  // namespace kml

@@ -55,6 +55,9 @@ struct BpLaunch {
 };
 
 // Returns hipSuccess or an error; `err` is set for configuration problems.
+// Dispatches to the static-assignment LDS kernel (bp_static.hip) when the code
+// fits it, else to the generic kernel (bp.hip).
+hipError_t launch_bp_static(const DevCode &c, const BpLaunch &a, hipStream_t s);
 hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const char **err);
 // Workspace the BP launcher needs in global-slot mode (double2 elements).
 long long bp_gslots_needed(const DevCode &c);
@@ -98,5 +101,8 @@ hipError_t launch_count_bytes(const uint8_t *uu, const uint8_t *uu_hat, int K, i
 
 // Device-side self tests of the exact-math helpers (hypot, complex division).
 hipError_t launch_math_probe(const double *in, int n, double *out, hipStream_t s);
+// Device-side self test of the shared-reciprocal division (bp_common.hpp):
+// in[n][3] = (n0, n1, s) -> out[n][4] = (fast q0, fast q1, IEEE q0, IEEE q1).
+hipError_t launch_div_probe(const double *in, int n, double *out, hipStream_t s);
 
 }  // namespace kml

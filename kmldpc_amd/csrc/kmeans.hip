@@ -19,6 +19,7 @@
 // floating-point chain in ascending symbol order (its rounding is part of the
 // result), so the parallelism has to come from independent codewords, not from
 // splitting a codeword's symbols.  A wavefront carries 64 independent chains.
+#include "bp_common.hpp"
 #include "exact_math.hpp"
 #include "kernels.hpp"
 
@@ -123,7 +124,25 @@ __global__ void math_probe_kernel(const double *in, int n, double *out) {
   out[4 * i + 2] = q.im;
   out[4 * i + 3] = kml_exp(a);
 }
+__global__ void div_probe_kernel(const double *in, int n, double *out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double n0 = in[3 * i], n1 = in[3 * i + 1], s = in[3 * i + 2];
+  double q0, q1, r0, r1;
+  div2<true>(n0, n1, s, q0, q1);
+  div2<false>(n0, n1, s, r0, r1);
+  out[4 * i] = q0;
+  out[4 * i + 1] = q1;
+  out[4 * i + 2] = r0;
+  out[4 * i + 3] = r1;
+}
 }  // namespace
+
+hipError_t launch_div_probe(const double *in, int n, double *out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(div_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_math_probe(const double *in, int n, double *out, hipStream_t s) {
   if (n == 0) return hipSuccess;

@@ -88,6 +88,29 @@ def test_device_exp_vs_glibc(data_dir):
     assert np.array_equal(out, ref)
 
 
+def test_fast_division_is_ieee_exact(data_dir):
+    """The decoder's shared-reciprocal division pair (bp_common.hpp div2) equals
+    two IEEE divisions over the value domain it is used on: numerators in
+    {0} U [2^-840, 1], s = n0 + n1 (the normalisations of the BP chains)."""
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    rng = np.random.default_rng(7)
+    for scale_exp in (1, 8, 40, 200, 840):
+        n = 400000
+        n0 = rng.random(n) * 2.0 ** -rng.uniform(0, scale_exp, n)
+        n1 = rng.random(n) * 2.0 ** -rng.uniform(0, scale_exp, n)
+        n0[::97] = 0.0
+        n1[1::89] = 0.0
+        n0 = np.where(n0 < 2.0 ** -840, 0.0, n0)
+        n1 = np.where(n1 < 2.0 ** -840, 0.0, n1)
+        s = n0 + n1
+        keep = s > 0
+        x = np.stack([n0[keep], n1[keep], s[keep]], axis=1)
+        out = ctx.div_probe(x)
+        assert np.array_equal(out[:, 2], x[:, 0] / x[:, 2])  # device IEEE == numpy IEEE
+        assert np.array_equal(out[:, 0], out[:, 2]), scale_exp
+        assert np.array_equal(out[:, 1], out[:, 3]), scale_exp
+
+
 @pytest.mark.parametrize("case", CASES)
 def test_bp_golden_vectors(case, data_dir):
     """Decode the reference's own P0 vectors: every output bit-exact."""
