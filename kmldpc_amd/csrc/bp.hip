@@ -290,13 +290,16 @@ hipError_t dispatch_deg(const DevCode &c, const BpLaunch &a, unsigned int *queue
 }  // namespace
 
 namespace {
-bool force_generic() {
+// KML_BP_KERNEL=generic|static forces a kernel family (A/B measurements).
+int kernel_variant() {
   static int v = -1;
   if (v < 0) {
-    const char *e = getenv("KML_BP_GENERIC");
-    v = (e && e[0] == '1') ? 1 : 0;
+    const char *e = getenv("KML_BP_KERNEL");
+    v = 0;
+    if (e && e[0] == 'g') v = 1;
+    if (e && e[0] == 's') v = 2;
   }
-  return v == 1;
+  return v;
 }
 }  // namespace
 
@@ -322,7 +325,12 @@ hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const c
     return hipErrorInvalidValue;
   }
   const bool lds = bp_uses_lds(c);
-  if (lds && !force_generic()) {
+  const int variant = kernel_variant();  // 0 auto, 1 generic, 2 static
+  if (lds && variant == 0) {
+    hipError_t e = launch_bp_regular(c, a, s);
+    if (e != hipErrorNotSupported) return e;
+  }
+  if (lds && variant != 1) {
     hipError_t e = launch_bp_static(c, a, s);
     if (e != hipErrorNotSupported) return e;
   }

@@ -1,0 +1,305 @@
+// bp_regular.hip — BP decoder specialised for regular (dv, dc) codes whose
+// message state fits in LDS (PEG2304: dv = 3, dc = 6, 6912 edges).
+//
+// Arithmetic: bit-exact restatement of lab::BinaryLDPCCodec::Decoder
+// (lib/lab/src/binaryldpccodec.cc:165-278), like bp.hip / bp_static.hip.
+//
+// Mapping onto a gfx950 CU (one workgroup of T threads per CU, all message
+// slots in LDS, persistent over codewords via a dequeue counter):
+//   * VN phase: thread t owns columns vn_order[r*T + t], r < RV, exactly
+//     (N == RV*T): no predicates, RV independent chains per thread.
+//   * CN phase: every check row is shared by an adjacent lane PAIR.  The even
+//     lane runs the forward trellis (alpha, binaryldpccodec.cc:237-249) over the
+//     row's v2c messages, the odd lane the backward trellis (beta, :251-273)
+//     over the same messages in reverse; the lanes then swap the chain states
+//     they need through one DPP quad_perm per word, and each computes half of
+//     the row's c2v outputs.  c2v_k = clip(t0 / (t0 + t1)) with
+//     t0 = a0*b0 + a1*b1, t1 = a0*b1 + a1*b0 is symmetric in (alpha_k, beta_k)
+//     under IEEE arithmetic (products commute, the two-term sums commute), so
+//     both lanes evaluate the same formula on (own state, partner state) and
+//     the result is the reference's bit for bit.  2M == RC*T half-rows:
+//     the CN phase has exactly as many lanes busy as the VN phase.
+//   * the early-stop parity check XORs the two half-rows through the same DPP
+//     swap.
+#include "bp_common.hpp"
+#include "kernels.hpp"
+
+namespace kml {
+
+namespace {
+
+constexpr int kRedBytes = 16;
+
+// swap a double with the adjacent lane (quad_perm [1,0,3,2])
+__device__ __forceinline__ double swap_pair(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  const int lo2 = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false);
+  const int hi2 = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
+  return __hiloint2double(hi2, lo2);
+}
+__device__ __forceinline__ int swap_pair_i(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }
+
+template <int T, int RV, int RC, int DV, int DC, bool SYN, bool FAST>
+__device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, int cw, double2 *slots,
+                                           unsigned char *cch, const int (&vcol)[RV], const int (&vslot)[RV][DV],
+                                           const double (&pv)[RV], const int (&crow)[RC], const int (&cbase)[RC],
+                                           const int (&ccol)[RC][(DC + 1) / 2], int odd, int &iter_out,
+                                           bool &conv_out) {
+  constexpr int H = (DC + 1) / 2;  // edges per half-row (upper half incl. middle for the odd lane)
+  int iter = 0;
+  bool conv = false;
+  for (; iter < a.iter_count; ++iter) {
+    // ------------------------------------------------------------ VN phase
+    {
+      double c0s[RV][DV];
+#pragma unroll
+      for (int r = 0; r < RV; ++r)
+#pragma unroll
+        for (int k = 0; k < DV; ++k) c0s[r][k] = slots[vslot[r][k]].x;
+#pragma unroll
+      for (int r = 0; r < RV; ++r) {
+        double a0 = pv[r], a1 = 1.0 - pv[r];
+        double al0[DV], al1[DV];
+#pragma unroll
+        for (int k = 0; k < DV; ++k) {
+          al0[k] = a0;
+          al1[k] = a1;
+          const double c0 = c0s[r][k];
+          const double n0 = a0 * c0;
+          const double n1 = a1 * (1.0 - c0);
+          div2<FAST>(n0, n1, n0 + n1, a0, a1);
+        }
+        cch[vcol[r]] = (a0 > a1) ? 0 : 1;
+        double b0 = 1.0, b1 = 1.0;
+#pragma unroll
+        for (int k = DV - 1; k >= 0; --k) {
+          const double t0 = al0[k] * b0;
+          const double t1 = al1[k] * b1;
+          double q0, q1;
+          div2<FAST>(t0, t1, t0 + t1, q0, q1);
+          slots[vslot[r][k]] = make_double2(q0, q1);
+          if (k > 0) {
+            const double c0 = c0s[r][k];
+            const double n0 = b0 * c0;
+            const double n1 = b1 * (1.0 - c0);
+            div2<FAST>(n0, n1, n0 + n1, b0, b1);
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ------------------------------------------------ early-stop parity check
+    int fail = 0;
+#pragma unroll
+    for (int r = 0; r < RC; ++r) {
+      int p = 0;
+#pragma unroll
+      for (int k = 0; k < H; ++k)
+        if (odd || k < DC / 2) p ^= cch[ccol[r][k]];  // middle edge of an odd row: odd lane only
+      fail |= p ^ swap_pair_i(p);
+    }
+    if (!__syncthreads_or(fail)) {
+      conv = true;
+      break;
+    }
+
+    // ------------------------------------------------------------ CN phase
+    {
+      // own-order messages: even lane k = s, odd lane k = DC-1-s
+      double v0[RC][DC], v1[RC][DC];
+#pragma unroll
+      for (int r = 0; r < RC; ++r)
+#pragma unroll
+        for (int s = 0; s < DC; ++s) {
+          const double2 m = slots[cbase[r] + (odd ? DC - 1 - s : s)];
+          v0[r][s] = m.x;
+          v1[r][s] = m.y;
+        }
+#pragma unroll
+      for (int r = 0; r < RC; ++r) {
+        // chain: even lane = alpha (forward), odd lane = beta (backward)
+        double x0[DC], x1[DC];
+        double a0 = 1.0, a1 = 0.0;
+#pragma unroll
+        for (int s = 0; s < DC; ++s) {
+          x0[s] = a0;
+          x1[s] = a1;
+          if (SYN || s + 1 < DC) {
+            const double n0 = a0 * v0[r][s] + a1 * v1[r][s];
+            const double n1 = a0 * v1[r][s] + a1 * v0[r][s];
+            div2<FAST>(n0, n1, n0 + n1, a0, a1);
+          }
+        }
+        if constexpr (SYN)
+          if (!odd) a.syn[(long long)cw * c.M + crow[r]] = a0;  // alpha past the last edge (:274)
+        // exchange + c2v for the own half: j in [DC/2, DC)
+#pragma unroll
+        for (int j = DC / 2; j < DC; ++j) {
+          const double y0 = swap_pair(x0[j]);
+          const double y1 = swap_pair(x1[j]);
+          const double o0 = x0[DC - 1 - j], o1 = x1[DC - 1 - j];
+          const double t0 = o0 * y0 + o1 * y1;
+          const double t1 = o0 * y1 + o1 * y0;
+          double q = div1<FAST>(t0, t0 + t1);
+          if (q > 1.0 - kSmallestProb) q = 1.0 - kSmallestProb;
+          if (q < kSmallestProb) q = kSmallestProb;
+          slots[cbase[r] + (odd ? j : DC - 1 - j)].x = q;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  iter_out = iter;
+  conv_out = conv;
+}
+
+template <int T, int RV, int RC, int DV, int DC, bool SYN>
+__global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, unsigned int *queue, int fast_allowed) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int H = (DC + 1) / 2;
+  const int tid = threadIdx.x;
+  const int odd = tid & 1;
+  double2 *slots = reinterpret_cast<double2 *>(smem);
+  int *red = reinterpret_cast<int *>(smem + (size_t)c.E * 16);
+  unsigned char *cch = smem + (size_t)c.E * 16 + kRedBytes;
+
+  int vcol[RV], vslot[RV][DV];
+#pragma unroll
+  for (int r = 0; r < RV; ++r) {
+    const int v = c.vn_order[r * T + tid];
+    const int b = c.col_ptr[v];
+    vcol[r] = v;
+#pragma unroll
+    for (int k = 0; k < DV; ++k) vslot[r][k] = c.col_slot[b + k];
+  }
+  int crow[RC], cbase[RC], ccol[RC][H];
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int row = c.cn_order[r * (T / 2) + (tid >> 1)];
+    crow[r] = row;
+    cbase[r] = c.row_ptr[row];
+#pragma unroll
+    for (int k = 0; k < H; ++k) {  // parity columns: even lane edges [0, DC/2), odd lane [DC/2, DC)
+      const int e = odd ? DC / 2 + k : k;
+      ccol[r][k] = c.row_col[cbase[r] + (e < DC ? e : DC - 1)];
+    }
+  }
+
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) {
+      red[3] = (int)atomicAdd(queue, 1u);
+      red[0] = 0;
+      red[1] = 0;
+    }
+    __syncthreads();
+    const int cw = red[3];
+    if (cw >= a.B) break;
+    const double *p0 = a.p0 + (long long)cw * a.p0_stride;
+    if (a.p0_sel) p0 += (long long)a.p0_sel[cw] * a.p0_sel_stride;
+
+    double pv[RV];
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < RV; ++r) {
+      pv[r] = (vcol[r] >= c.punct) ? p0[vcol[r] - c.punct] : 0.5;
+      ok = ok && fast_prior_ok(pv[r]);
+    }
+    for (int e = tid; e < c.E; e += T) slots[e].x = 0.5;  // InitMsg
+    const bool fast = __syncthreads_and(ok ? 1 : 0) && fast_allowed;
+
+    int iter = 0;
+    bool conv = false;
+    if (fast)
+      decode_reg<T, RV, RC, DV, DC, SYN, true>(c, a, cw, slots, cch, vcol, vslot, pv, crow, cbase, ccol, odd, iter,
+                                              conv);
+    else
+      decode_reg<T, RV, RC, DV, DC, SYN, false>(c, a, cw, slots, cch, vcol, vslot, pv, crow, cbase, ccol, odd, iter,
+                                               conv);
+
+    if (a.iter_count > 0) {
+      if (a.uu_hat) {
+        uint8_t *u = a.uu_hat + (long long)cw * c.K;
+        for (int i = tid; i < c.K; i += T) u[i] = cch[i + c.info_off];
+      }
+      if (a.cc_hat) {
+        uint8_t *o = a.cc_hat + (long long)cw * c.N;
+        for (int v = tid; v < c.N; v += T) o[v] = cch[v];
+      }
+      if (a.parity_cnt) {
+        int cnt = 0;
+#pragma unroll
+        for (int r = 0; r < RC; ++r) {
+          int p = 0;
+#pragma unroll
+          for (int k = 0; k < H; ++k)
+            if (odd || k < DC / 2) p ^= cch[ccol[r][k]];
+          const int full = p ^ swap_pair_i(p);
+          if (!odd) cnt += full;
+        }
+        if (cnt) atomicAdd(&red[0], cnt);
+      }
+      if (a.ref_bits) {
+        const uint64_t *ref = a.ref_bits + (long long)cw * c.Kw;
+        int errs = 0;
+        for (int w = tid; w < c.Kw; w += T) {
+          uint64_t word = 0;
+          const int base = w * 64;
+          const int nb = min(64, c.K - base);
+          for (int j = 0; j < nb; ++j) word |= (uint64_t)cch[c.info_off + base + j] << j;
+          errs += __popcll(word ^ ref[w]);
+        }
+        if (errs) atomicAdd(&red[1], errs);
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      if (a.ret) a.ret[cw] = iter + (iter < a.max_iter);
+      if (a.parity_cnt) a.parity_cnt[cw] = red[0];
+      if (a.counters) {
+        const unsigned long long vn = conv ? (unsigned long long)iter + 1 : (unsigned long long)iter;
+        atomicAdd(&a.counters[CNT_VN_PHASES], vn);
+        atomicAdd(&a.counters[CNT_CN_PHASES], (unsigned long long)iter);
+        if (conv) atomicAdd(&a.counters[CNT_CONVERGED], 1ull);
+        if (a.ref_bits && a.iter_count > 0) {
+          const int errs = red[1];
+          atomicAdd(&a.counters[CNT_ERR_BIT], (unsigned long long)errs);
+          atomicAdd(&a.counters[CNT_ERR_BLK], errs > 0 ? 1ull : 0ull);
+          atomicAdd(&a.counters[CNT_TOT_BIT], (unsigned long long)c.K);
+          atomicAdd(&a.counters[CNT_TOT_BLK], 1ull);
+        }
+      }
+    }
+  }
+}
+
+template <int T, int RV, int RC, int DV, int DC, bool SYN>
+hipError_t launch_reg_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
+  auto kern = bp_regular_kernel<T, RV, RC, DV, DC, SYN>;
+  const size_t lds = (size_t)c.E * 16 + kRedBytes + (size_t)c.N;
+  hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  int dev = 0, ncu = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  long long grid = ncu;
+  if (grid > a.B) grid = a.B;
+  e = hipMemsetAsync(a.queue, 0, sizeof(unsigned int), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(T), lds, s, c, a, a.queue, fast_allowed);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s) {
+  if (!c.regular || (long long)c.E * 16 + kRedBytes + c.N > 160 * 1024) return hipErrorNotSupported;
+  const int fast = c.dv_max <= kFastMaxColumnDegree ? 1 : 0;
+  // PEG2304-class: dv 3, dc 6, N = 3*768, 2M = 3*768
+  if (c.dv_max == 3 && c.dc_max == 6 && c.N == 3 * 768 && 2 * c.M == 3 * 768)
+    return a.syn ? launch_reg_t<768, 3, 3, 3, 6, true>(c, a, s, fast) : launch_reg_t<768, 3, 3, 3, 6, false>(c, a, s, fast);
+  return hipErrorNotSupported;
+}
+
+}  // namespace kml

@@ -26,7 +26,7 @@ namespace {
 
 constexpr int kRedBytes = 16;
 
-template <int T, int RV, int RC, int DV, int DC, bool SYN, bool FAST>
+template <int T, int RV, int RC, int DV, int DC, bool REG, bool SYN, bool FAST>
 __device__ __forceinline__ void decode_cw(const DevCode &c, const BpLaunch &a, int cw, double2 *slots,
                                           unsigned char *cch, const int (&vcol)[RV], const int (&vdeg)[RV],
                                           const int (&vslot)[RV][DV], const double (&pv)[RV], const int (&crow)[RC],
@@ -41,10 +41,11 @@ __device__ __forceinline__ void decode_cw(const DevCode &c, const BpLaunch &a, i
 #pragma unroll
       for (int r = 0; r < RV; ++r)
 #pragma unroll
-        for (int k = 0; k < DV; ++k) c0s[r][k] = (k < vdeg[r]) ? slots[vslot[r][k]].x : 0.5;
+        for (int k = 0; k < DV; ++k) c0s[r][k] = (k < (REG ? (vcol[r] >= 0 ? DV : 0) : vdeg[r])) ? slots[vslot[r][k]].x : 0.5;
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
-        const int d = vdeg[r];
+        if (REG && vcol[r] < 0) continue;  // wave-uniform (only the tail round can be partial)
+        const int d = REG ? DV : vdeg[r];
         double a0 = pv[r], a1 = 1.0 - pv[r];
         double al0[DV], al1[DV];
 #pragma unroll
@@ -103,13 +104,14 @@ __device__ __forceinline__ void decode_cw(const DevCode &c, const BpLaunch &a, i
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
           double2 m = make_double2(0.5, 0.5);
-          if (k < cdeg[r]) m = slots[cbase[r] + k];
+          if (k < (REG ? (crow[r] >= 0 ? DC : 0) : cdeg[r])) m = slots[cbase[r] + k];
           v0[r][k] = m.x;
           v1[r][k] = m.y;
         }
 #pragma unroll
       for (int r = 0; r < RC; ++r) {
-        const int d = cdeg[r];
+        if (REG && crow[r] < 0) continue;
+        const int d = REG ? DC : cdeg[r];
         double al0[DC], al1[DC];
         double a0 = 1.0, a1 = 0.0;
 #pragma unroll
@@ -149,7 +151,7 @@ __device__ __forceinline__ void decode_cw(const DevCode &c, const BpLaunch &a, i
   conv_out = conv;
 }
 
-template <int T, int RV, int RC, int DV, int DC, bool SYN>
+template <int T, int RV, int RC, int DV, int DC, bool REG, bool SYN>
 __global__ __launch_bounds__(T) void bp_static_kernel(DevCode c, BpLaunch a, unsigned int *queue, int fast_allowed) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
@@ -219,10 +221,10 @@ __global__ __launch_bounds__(T) void bp_static_kernel(DevCode c, BpLaunch a, uns
     int iter = 0;
     bool conv = false;
     if (fast)
-      decode_cw<T, RV, RC, DV, DC, SYN, true>(c, a, cw, slots, cch, vcol, vdeg, vslot, pv, crow, cbase, cdeg, ccol,
+      decode_cw<T, RV, RC, DV, DC, REG, SYN, true>(c, a, cw, slots, cch, vcol, vdeg, vslot, pv, crow, cbase, cdeg, ccol,
                                              iter, conv);
     else
-      decode_cw<T, RV, RC, DV, DC, SYN, false>(c, a, cw, slots, cch, vcol, vdeg, vslot, pv, crow, cbase, cdeg, ccol,
+      decode_cw<T, RV, RC, DV, DC, REG, SYN, false>(c, a, cw, slots, cch, vcol, vdeg, vslot, pv, crow, cbase, cdeg, ccol,
                                               iter, conv);
 
     // ---------------- epilogue (same contract as bp.hip)
@@ -281,9 +283,9 @@ __global__ __launch_bounds__(T) void bp_static_kernel(DevCode c, BpLaunch a, uns
   }
 }
 
-template <int T, int RV, int RC, int DV, int DC, bool SYN>
+template <int T, int RV, int RC, int DV, int DC, bool REG, bool SYN>
 hipError_t launch_static_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
-  auto kern = bp_static_kernel<T, RV, RC, DV, DC, SYN>;
+  auto kern = bp_static_kernel<T, RV, RC, DV, DC, REG, SYN>;
   const size_t lds = (size_t)c.E * 16 + kRedBytes + (size_t)c.N;
   hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -310,8 +312,13 @@ hipError_t launch_bp_static(const DevCode &c, const BpLaunch &a, hipStream_t s) 
   const int fast = c.dv_max <= kFastMaxColumnDegree ? 1 : 0;
   if ((long long)c.E * 16 + kRedBytes + c.N > 160 * 1024) return hipErrorNotSupported;
   if (rv <= 3 && rc <= 2) {
+    // regular (3,6) code: every column has degree 3 and every row degree 6
+    if (c.regular && c.dv_max == 3 && c.dc_max == 6)
+      return a.syn ? launch_static_t<T, 3, 2, 3, 6, true, true>(c, a, s, fast)
+                   : launch_static_t<T, 3, 2, 3, 6, true, false>(c, a, s, fast);
     if (c.dv_max <= 3 && c.dc_max <= 6)
-      return a.syn ? launch_static_t<T, 3, 2, 3, 6, true>(c, a, s, fast) : launch_static_t<T, 3, 2, 3, 6, false>(c, a, s, fast);
+      return a.syn ? launch_static_t<T, 3, 2, 3, 6, false, true>(c, a, s, fast)
+                   : launch_static_t<T, 3, 2, 3, 6, false, false>(c, a, s, fast);
   }
   return hipErrorNotSupported;
 }

@@ -153,6 +153,11 @@ int upload_code(kml_ctx *c) {
   d.dc_max = L.dc_max;
   d.is5g = L.is5g ? 1 : 0;
   d.active = L.active ? 1 : 0;
+  d.regular = 1;
+  for (int j = 0; j < L.N; j++)
+    if (L.col_ptr[j + 1] - L.col_ptr[j] != L.dv_max) d.regular = 0;
+  for (int i = 0; i < L.M; i++)
+    if (L.row_ptr[i + 1] - L.row_ptr[i] != L.dc_max) d.regular = 0;
 
   HIPCHK(c, c->d_cons.ensure(sizeof(double) * (c->modem.pts.size() + 8)), "hipMalloc(cons)");
   kml::rotation_factors(c->rot);

@@ -21,6 +21,7 @@ struct DevCode {
   const int32_t *row_ptr, *row_col, *col_ptr, *col_slot, *vn_order, *cn_order;
   const uint64_t *enc_info;
   int M, N, E, K, cc_len, punct, info_off, chk, Kw, dv_max, dc_max, is5g, active;
+  int regular;  // every column has degree dv_max and every row dc_max
 };
 
 // Counter block in device memory (uint64):
@@ -58,6 +59,7 @@ struct BpLaunch {
 // Dispatches to the static-assignment LDS kernel (bp_static.hip) when the code
 // fits it, else to the generic kernel (bp.hip).
 hipError_t launch_bp_static(const DevCode &c, const BpLaunch &a, hipStream_t s);
+hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s);
 hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const char **err);
 // Workspace the BP launcher needs in global-slot mode (double2 elements).
 long long bp_gslots_needed(const DevCode &c);
