@@ -146,6 +146,8 @@ int kml_sim_frames(kml_ctx *ctx, uint8_t *uu, double *y, double *h);
 int kml_prof_enable(kml_ctx *ctx, int on);
 int kml_prof_reset(kml_ctx *ctx);
 int kml_prof_read(kml_ctx *ctx, const char *stage, int64_t *launches, double *total_ms, double *alg_bytes);
+/* Summed algorithmic fp64 flops of the stage's launches ("bp" only). */
+int kml_prof_read_flops(kml_ctx *ctx, const char *stage, double *alg_flops);
 
 /* Device-side probe of the exact-math helpers: in[n][4] = (a, b, c, d) ->
  * out[n][4] = (hypot(a,b), re((a+ib)/(c+id)), im(...), exp(a)) with the

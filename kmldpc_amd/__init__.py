@@ -69,6 +69,7 @@ def lib():
         "kml_prof_enable": (I, [P, I]),
         "kml_prof_reset": (I, [P]),
         "kml_prof_read": (I, [P, C.c_char_p, P, P, P]),
+        "kml_prof_read_flops": (I, [P, C.c_char_p, P]),
         "kml_math_probe": (I, [P, P, I, P]),
         "kml_div_probe": (I, [P, P, I, P]),
     }
@@ -261,8 +262,10 @@ class Context:
         n = np.zeros(1, np.int64)
         ms = np.zeros(1)
         by = np.zeros(1)
+        fl = np.zeros(1)
         self._chk(lib().kml_prof_read(self._h, stage.encode(), _p(n), _p(ms), _p(by)), "kml_prof_read")
-        return dict(launches=int(n[0]), ms=float(ms[0]), bytes=float(by[0]))
+        self._chk(lib().kml_prof_read_flops(self._h, stage.encode(), _p(fl)), "kml_prof_read_flops")
+        return dict(launches=int(n[0]), ms=float(ms[0]), bytes=float(by[0]), flops=float(fl[0]))
 
     def div_probe(self, x):
         x = _f64(x).reshape(-1, 3)

@@ -50,7 +50,7 @@ struct Pending {
 
 struct Stat {
   int64_t launches = 0;
-  double ms = 0, bytes = 0;
+  double ms = 0, bytes = 0, flops = 0;
 };
 
 constexpr int kArenaSlots = 1024;
@@ -67,6 +67,8 @@ struct kml_ctx {
   double rot[8];
   // resident constants
   DBuf d_graph, d_cons;
+  // algorithmic fp64 flops per executed VN / CN phase ("Roofline")
+  double vn_flops = 0, cn_flops = 0;
   DBuf d_arena;  // kArenaSlots x CNT_N counters
   int arena_next = 0;
   DBuf d_queue, d_gslots;
@@ -174,9 +176,23 @@ int upload_code(kml_ctx *c) {
   return KML_OK;
 }
 
+// FP64 work of one VN / CN phase of the exact algorithm: per column of degree
+// d, 68d - 23 flops; per row of degree d, 73d - 52 flops (fma = 2, mul / add /
+// sub / rcp = 1; each normalisation pair = one reciprocal refinement + two
+// residual corrections, the minimal exact-IEEE sequence).
+void phase_flops(kml_ctx *c) {
+  const kml::LdpcCode &L = c->code;
+  double v = 0, r = 0;
+  for (int j = 0; j < L.N; j++) v += 68.0 * (L.col_ptr[j + 1] - L.col_ptr[j]) - 23.0;
+  for (int i = 0; i < L.M; i++) r += 73.0 * (L.row_ptr[i + 1] - L.row_ptr[i]) - 52.0;
+  c->vn_flops = v;
+  c->cn_flops = r;
+}
+
 int finish_create(kml_ctx *c) {
   std::string err;
   if (!c->code.load(c->rc.matrix_file, c->rc.is5g, c->rc.active, false, err)) return fail(c, KML_E_IO, err);
+  phase_flops(c);
   if (!c->modem.load(c->rc.modem_file, err)) return fail(c, KML_E_IO, err);
   if (c->code.cc_len % c->modem.bits != 0)  // modemlinearsystem.cc:7-12
     return fail(c, KML_E_ARG, "(cc_len = " + std::to_string(c->code.cc_len) + ") % (input_len = " +
@@ -238,6 +254,11 @@ void drain_profile(kml_ctx *c) {
       bytes += (double)h[kml::CNT_VN_PHASES] * (24.0 * E + 9.0 * N) + (double)h[kml::CNT_CN_PHASES] * 24.0 * E;
     }
     s.bytes += bytes;
+    if (p.cnt_slot >= 0) {
+      unsigned long long h[kml::CNT_N];
+      hipMemcpy(h, slot_ptr(c, p.cnt_slot), sizeof(h), hipMemcpyDeviceToHost);
+      s.flops += (double)h[kml::CNT_VN_PHASES] * c->vn_flops + (double)h[kml::CNT_CN_PHASES] * c->cn_flops;
+    }
     hipEventDestroy(p.ev0);
     hipEventDestroy(p.ev1);
   }
@@ -732,6 +753,15 @@ int kml_prof_reset(kml_ctx *c) {
   if (!c) return KML_E_ARG;
   drain_profile(c);
   c->stats.clear();
+  return KML_OK;
+}
+
+int kml_prof_read_flops(kml_ctx *c, const char *stage, double *alg_flops) {
+  if (!c || !stage || !alg_flops) return KML_E_ARG;
+  if (c->device >= 0) hipSetDevice(c->device);
+  drain_profile(c);
+  auto it = c->stats.find(stage);
+  *alg_flops = it != c->stats.end() ? it->second.flops : 0.0;
   return KML_OK;
 }
 
