@@ -74,7 +74,7 @@ struct kml_ctx {
   DBuf d_queue, d_gslots;
   long long gslots_cap = 0;
   // workspaces
-  DBuf w_y, w_h, w_h4, w_hhat, w_p0, w_uu, w_uh, w_ret, w_cch, w_syn, w_sel, w_met, w_pc, w_cnt;
+  DBuf w_y, w_h, w_h4, w_hhat, w_p0, w_uu, w_uh, w_ret, w_cch, w_syn, w_sel, w_met, w_pc, w_cnt, w_km;
   // resident simulation frames
   DBuf s_uu, s_cc, s_y, s_h;
   int sim_B = 0;
@@ -368,8 +368,10 @@ int receive(kml_ctx *c, const double2 *y, const double2 *true_h, double snr, int
     hh = c->w_hhat.as<double2>();
   }
   {
+    HIPCHK(c, c->w_km.ensure(kml::kmeans_workspace_bytes(S, B)), "hipMalloc(kmeans)");
     Timer t(c, "kmeans", -1, (double)B * S * 16.0);
-    HIPCHK(c, kml::launch_kmeans(c->modem.Kc, cons, rot, y, S, 20, B, hh, c->w_h4.as<double2>(), c->stream), "kmeans");
+    HIPCHK(c, kml::launch_kmeans(c->modem.Kc, cons, rot, y, S, 20, B, hh, c->w_h4.as<double2>(), c->w_km.p, c->stream),
+           "kmeans");
     t.stop();
   }
   int32_t *chosen = d_chosen;
@@ -474,7 +476,7 @@ void kml_destroy(kml_ctx *c) {
     drain_profile(c);
     for (DBuf *b : {&c->d_graph, &c->d_cons, &c->d_arena, &c->d_queue, &c->d_gslots, &c->w_y, &c->w_h, &c->w_h4,
                     &c->w_hhat, &c->w_p0, &c->w_uu, &c->w_uh, &c->w_ret, &c->w_cch, &c->w_syn, &c->w_sel, &c->w_met,
-                    &c->w_pc, &c->w_cnt, &c->s_uu, &c->s_cc, &c->s_y, &c->s_h})
+                    &c->w_pc, &c->w_cnt, &c->w_km, &c->s_uu, &c->s_cc, &c->s_y, &c->s_h})
       b->release();
     hipStreamDestroy(c->stream);
   }
@@ -604,10 +606,11 @@ int kml_kmeans(kml_ctx *c, const double *y, int B, int iters, double *h_hat, dou
   d_hh = (h_hat && (flags & KML_DEVICE_PTRS)) ? h_hat : c->w_hhat.as<double>();
   d_h4 = (h4 && (flags & KML_DEVICE_PTRS)) ? h4 : c->w_h4.as<double>();
   const double *cons = c->d_cons.as<double>();
+  HIPCHK(c, c->w_km.ensure(kml::kmeans_workspace_bytes(S, B)), "hipMalloc(kmeans)");
   Timer t(c, "kmeans", -1, (double)B * S * 16.0);
   HIPCHK(c, kml::launch_kmeans(c->modem.Kc, cons, cons + c->modem.pts.size(), reinterpret_cast<const double2 *>(d_y), S,
                                iters, B, reinterpret_cast<double2 *>(d_hh), reinterpret_cast<double2 *>(d_h4),
-                               c->stream),
+                               c->w_km.p, c->stream),
          "kmeans");
   t.stop();
   TRY(copy_out(c, h_hat, (const double *)d_hh, (size_t)B * 2, flags));

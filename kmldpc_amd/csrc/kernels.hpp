@@ -80,9 +80,14 @@ hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, co
 // argmin over a [B][4] metric table (first minimum) for the BP-based metrics.
 hipError_t launch_select(const int32_t *parity_cnt, int B, double *metrics, int32_t *chosen, hipStream_t s);
 
-// KMeans::Run + h_hat = clusters[0]/c[0] + 4 rotations, one lane per codeword.
+// KMeans::Run + h_hat = clusters[0]/c[0] + 4 rotations (kmeans.hip).
+struct KmState {
+  double2 hat, prev, sum;  // current h_hat, previous iteration's, cumulative cluster-0 sum
+  int cnt, it, done, have_prev;
+};
+size_t kmeans_workspace_bytes(int S, int B);
 hipError_t launch_kmeans(int Kc, const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
-                         double2 *h_hat, double2 *h4, hipStream_t s);
+                         double2 *h_hat, double2 *h4, void *ws, hipStream_t s);
 
 // GPU frame generation (counter-based Philox; statistically equivalent to the
 // reference's sequential Park-Miller stream, not bit-equal).

@@ -11,14 +11,29 @@
 //     iteration's (kmeans.cc:47-56), and tempClusters starts at zero;
 //   * |z| is glibc hypot, '/' is __divdc3 Smith division, '*' is the naive
 //     complex product (exact_math.hpp).
-// Only cluster 0's running sum/count is ever read back, so that is all we keep;
-// the per-symbol assignment still evaluates every cluster to find the first
-// minimum (kmeans.cc:41-44).
+// Only cluster 0's running sum/count is ever read back, so the assignment only
+// has to decide, per symbol, whether cluster 0 is the FIRST minimum of the K
+// distances (kmeans.cc:41-44).
 //
-// Mapping: one LANE per codeword.  The cluster-0 sum is a sequential
-// floating-point chain in ascending symbol order (its rounding is part of the
-// result), so the parallelism has to come from independent codewords, not from
-// splitting a codeword's symbols.  A wavefront carries 64 independent chains.
+// MI355X mapping — one k-means iteration is two launches:
+//   km_assign  one thread per (codeword, symbol): the K distances are screened
+//              with squared norms d2 = dr*dr + di*di (relative error <= 3 ulp of
+//              the exact |.|^2 of the same rounded dr, di; glibc hypot is
+//              within 1 ulp of the exact |.|), so "cluster 0 is the strict
+//              unique minimum" / "some k beats cluster 0" is decided exactly
+//              whenever the d2 margin exceeds 1e-12 relative; inside that band
+//              the glibc-exact hypot decides, with the reference's first-minimum
+//              rule.  Non-finite or extreme d2 take the exact path.  The
+//              cluster points c[k]*h_hat are computed once per workgroup into
+//              LDS.  Membership bits are packed with a wavefront ballot.
+//   km_update  one LANE per codeword: walks the membership bits in ascending
+//              symbol order and adds the members' y to the running cluster-0
+//              sum — a sequential floating-point chain whose rounding is part
+//              of the result, so the parallelism comes from 64 codewords per
+//              wavefront — then the exact convergence test and the update
+//              (Smith divisions).
+// km_init (first max of |y|, same screening) and km_final (h_hat and the 4
+// rotated candidates) are lane-per-codeword.
 #include "bp_common.hpp"
 #include "exact_math.hpp"
 #include "kernels.hpp"
@@ -27,65 +42,197 @@ namespace kml {
 
 namespace {
 
-template <int KC>
-__global__ __launch_bounds__(64) void kmeans_kernel(const double *__restrict__ cons, const double *__restrict__ rot,
-                                                    const double2 *__restrict__ y, int S, int iters, int B,
-                                                    double2 *__restrict__ h_hat, double2 *__restrict__ h4) {
-  const int cw = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cw >= B) return;
-  const double2 *yy = y + (long long)cw * S;
-  const cplx c0{cons[0], cons[1]};
+constexpr double kTieBand = 1e-12;
+constexpr double kD2Lo = 1e-290, kD2Hi = 1e290;
 
-  // first max of |y| (kmeans.cc:17-22)
-  int mi = 0;
-  double best = kml_hypot(yy[0].x, yy[0].y);
-  for (int j = 1; j < S; ++j) {
+__device__ __forceinline__ bool d2_ok(double d) { return d >= kD2Lo && d <= kD2Hi; }
+
+// first max of |y_j| over j (kmeans.cc:17-22)
+__device__ int first_max_abs(const double2 *yy, int S) {
+  double best = -1.0;
+  bool exact = false;
+  for (int j = 0; j < S; ++j) {
     const double2 v = yy[j];
-    const double a = kml_hypot(v.x, v.y);
-    if (best < a) {
-      best = a;
+    const double d = v.x * v.x + v.y * v.y;
+    if (!d2_ok(d) && !(d == 0.0)) exact = true;
+    if (d > best) best = d;
+  }
+  if (!exact && best > 0.0) {
+    // candidates: d2 within the tie band of the maximum; the first exact max wins
+    int mi = -1;
+    double hb = 0.0;
+    for (int j = 0; j < S; ++j) {
+      const double2 v = yy[j];
+      const double d = v.x * v.x + v.y * v.y;
+      if (d >= best * (1.0 - kTieBand)) {
+        const double h = kml_hypot(v.x, v.y);
+        if (mi < 0 || hb < h) {
+          hb = h;
+          mi = j;
+        }
+      }
+    }
+    return mi;
+  }
+  // exact reference loop
+  int mi = 0;
+  double hb = kml_hypot(yy[0].x, yy[0].y);
+  for (int j = 1; j < S; ++j) {
+    const double h = kml_hypot(yy[j].x, yy[j].y);
+    if (hb < h) {
+      hb = h;
       mi = j;
     }
   }
-  cplx hat = kml_cdiv(cplx{yy[mi].x, yy[mi].y}, c0);  // kmeans.cc:25
-  cplx prev{0.0, 0.0};
-  bool have_prev = false;  // tempClusters starts as zeros
-  long long cnt0 = 0;
-  double s0r = 0.0, s0i = 0.0;
-  for (int it = 0; it < iters; ++it) {
-    for (int j = 0; j < S; ++j) {
-      const double2 v = yy[j];
-      const cplx cl0 = kml_cmul(c0, hat);
-      double dmin = kml_hypot(cl0.re - v.x, cl0.im - v.y);
-      int kmin = 0;
-#pragma unroll 4
-      for (int k = 1; k < KC; ++k) {
-        const cplx cl = kml_cmul(cplx{cons[2 * k], cons[2 * k + 1]}, hat);
-        const double d = kml_hypot(cl.re - v.x, cl.im - v.y);
-        if (d < dmin) {  // min_element: first minimum
-          dmin = d;
-          kmin = k;
-        }
-      }
-      if (kmin == 0) {
-        cnt0++;
-        s0r = s0r + v.x;
-        s0i = s0i + v.y;
-      }
-    }
-    bool same = true;  // kmeans.cc:47-56
-    for (int k = 0; k < KC && same; ++k) {
-      const cplx ck{cons[2 * k], cons[2 * k + 1]};
-      const cplx cl = kml_cmul(ck, hat);
-      const cplx tp = have_prev ? kml_cmul(ck, prev) : cplx{0.0, 0.0};
-      same = (cl.re == tp.re) && (cl.im == tp.im);
-    }
-    if (same) break;
-    prev = hat;
-    have_prev = true;
-    const cplx cl0 = kml_cdiv(cplx{s0r, s0i}, cplx{(double)(int)cnt0, 0.0});  // kmeans.cc:59-62
-    hat = kml_cdiv(cl0, c0);                                                 // kmeans.cc:64-71
+  return mi;
+}
+
+__global__ void km_init_kernel(const double *__restrict__ cons, const double2 *__restrict__ y, int S, int B,
+                               KmState *__restrict__ st) {
+  const int cw = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cw >= B) return;
+  const double2 *yy = y + (long long)cw * S;
+  const int mi = first_max_abs(yy, S);
+  const cplx hat = kml_cdiv(cplx{yy[mi].x, yy[mi].y}, cplx{cons[0], cons[1]});  // kmeans.cc:25
+  KmState s;
+  s.hat = make_double2(hat.re, hat.im);
+  s.prev = make_double2(0.0, 0.0);
+  s.sum = make_double2(0.0, 0.0);
+  s.cnt = 0;
+  s.it = 0;
+  s.done = 0;
+  s.have_prev = 0;
+  st[cw] = s;
+}
+
+// Is cluster 0 the first minimum of |c_k*hat - y| over k?  (kmeans.cc:41-44)
+template <int KC>
+__device__ __forceinline__ bool member0(const double2 *cl, double yr, double yi) {
+  double d0 = 0.0, m1 = 0.0;
+  bool fin = true;
+#pragma unroll 8
+  for (int k = 0; k < KC; ++k) {
+    const double2 c = cl[k];
+    const double dr = c.x - yr, di = c.y - yi;
+    const double d = dr * dr + di * di;
+    if (k == 0)
+      d0 = d;
+    else if (k == 1 || d < m1)
+      m1 = d;
+    fin = fin && d2_ok(d);
   }
+  if (fin) {
+    if (d0 < m1 * (1.0 - kTieBand)) return true;
+    if (d0 > m1 * (1.0 + kTieBand)) return false;
+    // near tie: glibc-exact distances of the contenders decide
+    const double h0 = kml_hypot(cl[0].x - yr, cl[0].y - yi);
+    for (int k = 1; k < KC; ++k) {
+      const double dr = cl[k].x - yr, di = cl[k].y - yi;
+      const double d = dr * dr + di * di;
+      if (d <= d0 * (1.0 + kTieBand))
+        if (kml_hypot(dr, di) < h0) return false;
+    }
+    return true;
+  }
+  // exact reference loop (non-finite or extreme magnitudes)
+  double hmin = kml_hypot(cl[0].x - yr, cl[0].y - yi);
+  int kmin = 0;
+  for (int k = 1; k < KC; ++k) {
+    const double h = kml_hypot(cl[k].x - yr, cl[k].y - yi);
+    if (h < hmin) {
+      hmin = h;
+      kmin = k;
+    }
+  }
+  return kmin == 0;
+}
+
+// grid: one workgroup per codeword; the workgroup's waves sweep its symbols in
+// 64-symbol words.
+template <int KC>
+__global__ __launch_bounds__(256) void km_assign_kernel(const double *__restrict__ cons, const double2 *__restrict__ y,
+                                                        int S, int Sw, const KmState *__restrict__ st,
+                                                        uint64_t *__restrict__ mem) {
+  __shared__ double2 cl[KC];
+  const int cw = blockIdx.x;
+  const KmState s = st[cw];
+  if (s.done) return;  // uniform per workgroup
+  const cplx hat{s.hat.x, s.hat.y};
+  for (int k = threadIdx.x; k < KC; k += blockDim.x) {
+    const cplx p = kml_cmul(cplx{cons[2 * k], cons[2 * k + 1]}, hat);  // clusters_[k] = c[k] * hatH
+    cl[k] = make_double2(p.re, p.im);
+  }
+  __syncthreads();
+  const double2 *yy = y + (long long)cw * S;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int w = wave; w < Sw; w += nw) {
+    const int j = w * 64 + lane;
+    bool m = false;
+    if (j < S) {
+      const double2 v = yy[j];
+      m = member0<KC>(cl, v.x, v.y);
+    }
+    const uint64_t bits = __ballot(m);
+    if (lane == 0) mem[(long long)cw * Sw + w] = bits;
+  }
+}
+
+template <int KC>
+__global__ void km_update_kernel(const double *__restrict__ cons, const double2 *__restrict__ y, int S, int Sw,
+                                 int iters, int B, KmState *__restrict__ st, const uint64_t *__restrict__ mem) {
+  const int cw = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cw >= B) return;
+  KmState s = st[cw];
+  if (s.done) return;
+  const double2 *yy = y + (long long)cw * S;
+  const uint64_t *mm = mem + (long long)cw * Sw;
+  // cumulative cluster-0 count and sum, ascending symbol order (kmeans.cc:36-46)
+  double sr = s.sum.x, si = s.sum.y;
+  int cnt = s.cnt;
+  for (int w = 0; w < Sw; ++w) {
+    uint64_t bits = mm[w];
+    while (bits) {
+      const int j = w * 64 + __builtin_ctzll(bits);
+      bits &= bits - 1;
+      const double2 v = yy[j];
+      sr = sr + v.x;
+      si = si + v.y;
+      cnt++;
+    }
+  }
+  s.sum = make_double2(sr, si);
+  s.cnt = cnt;
+  // convergence: every cluster equals the previous iteration's (kmeans.cc:47-56)
+  const cplx hat{s.hat.x, s.hat.y}, prev{s.prev.x, s.prev.y};
+  bool same = true;
+  for (int k = 0; k < KC && same; ++k) {
+    const cplx ck{cons[2 * k], cons[2 * k + 1]};
+    const cplx a = kml_cmul(ck, hat);
+    const cplx b = s.have_prev ? kml_cmul(ck, prev) : cplx{0.0, 0.0};
+    same = (a.re == b.re) && (a.im == b.im);
+  }
+  s.it++;
+  if (same) {
+    s.done = 1;
+  } else {
+    s.prev = s.hat;
+    s.have_prev = 1;
+    const cplx c0{cons[0], cons[1]};
+    const cplx m0 = kml_cdiv(cplx{sr, si}, cplx{(double)cnt, 0.0});  // kmeans.cc:59-62
+    const cplx nh = kml_cdiv(m0, c0);                                  // kmeans.cc:64-71
+    s.hat = make_double2(nh.re, nh.im);
+    if (s.it >= iters) s.done = 1;
+  }
+  st[cw] = s;
+}
+
+__global__ void km_final_kernel(const double *__restrict__ cons, const double *__restrict__ rot, int B,
+                                const KmState *__restrict__ st, double2 *__restrict__ h_hat,
+                                double2 *__restrict__ h4) {
+  const int cw = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cw >= B) return;
+  const cplx c0{cons[0], cons[1]};
+  const cplx hat{st[cw].hat.x, st[cw].hat.y};
   const cplx hh = kml_cdiv(kml_cmul(c0, hat), c0);  // simulator.cc:145
   h_hat[cw] = make_double2(hh.re, hh.im);
 #pragma unroll
@@ -95,24 +242,43 @@ __global__ __launch_bounds__(64) void kmeans_kernel(const double *__restrict__ c
   }
 }
 
-}  // namespace
-
-hipError_t launch_kmeans(int Kc, const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
-                         double2 *h_hat, double2 *h4, hipStream_t s) {
-  if (B == 0) return hipSuccess;
-  const dim3 grid((B + 63) / 64), blk(64);
-  switch (Kc) {
-    case 2: hipLaunchKernelGGL(kmeans_kernel<2>, grid, blk, 0, s, cons, rot, y, S, iters, B, h_hat, h4); break;
-    case 4: hipLaunchKernelGGL(kmeans_kernel<4>, grid, blk, 0, s, cons, rot, y, S, iters, B, h_hat, h4); break;
-    case 8: hipLaunchKernelGGL(kmeans_kernel<8>, grid, blk, 0, s, cons, rot, y, S, iters, B, h_hat, h4); break;
-    case 16: hipLaunchKernelGGL(kmeans_kernel<16>, grid, blk, 0, s, cons, rot, y, S, iters, B, h_hat, h4); break;
-    case 64: hipLaunchKernelGGL(kmeans_kernel<64>, grid, blk, 0, s, cons, rot, y, S, iters, B, h_hat, h4); break;
-    default: return hipErrorInvalidValue;
+template <int KC>
+hipError_t run_kmeans(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
+                      KmState *st, uint64_t *mem, double2 *h_hat, double2 *h4, hipStream_t s) {
+  const int Sw = (S + 63) / 64;
+  const dim3 lanes((B + 63) / 64), l64(64);
+  hipLaunchKernelGGL(km_init_kernel, lanes, l64, 0, s, cons, y, S, B, st);
+  const int threads = Sw >= 4 ? 256 : 64 * Sw;
+  for (int it = 0; it < iters; ++it) {
+    hipLaunchKernelGGL(km_assign_kernel<KC>, dim3(B), dim3(threads), 0, s, cons, y, S, Sw, st, mem);
+    hipLaunchKernelGGL(km_update_kernel<KC>, lanes, l64, 0, s, cons, y, S, Sw, iters, B, st, mem);
   }
+  hipLaunchKernelGGL(km_final_kernel, lanes, l64, 0, s, cons, rot, B, st, h_hat, h4);
   return hipGetLastError();
 }
 
-// Probe for the device restatements of hypot / complex division (tests).
+}  // namespace
+
+size_t kmeans_workspace_bytes(int S, int B) {
+  return (size_t)B * sizeof(KmState) + (size_t)B * ((S + 63) / 64) * sizeof(uint64_t) + 256;
+}
+
+hipError_t launch_kmeans(int Kc, const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
+                         double2 *h_hat, double2 *h4, void *ws, hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  KmState *st = reinterpret_cast<KmState *>(ws);
+  uint64_t *mem = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(ws) + (size_t)B * sizeof(KmState));
+  switch (Kc) {
+    case 2: return run_kmeans<2>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, s);
+    case 4: return run_kmeans<4>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, s);
+    case 8: return run_kmeans<8>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, s);
+    case 16: return run_kmeans<16>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, s);
+    case 64: return run_kmeans<64>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// Probe for the device restatements of hypot / complex division / exp (tests).
 namespace {
 __global__ void math_probe_kernel(const double *in, int n, double *out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -124,6 +290,7 @@ __global__ void math_probe_kernel(const double *in, int n, double *out) {
   out[4 * i + 2] = q.im;
   out[4 * i + 3] = kml_exp(a);
 }
+
 __global__ void div_probe_kernel(const double *in, int n, double *out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -189,6 +189,38 @@ def test_kmeans_vs_oracle(data_dir, matrix, modem, snr, n):
         assert np.array_equal(h4[i], O.rotations(ref)), i
 
 
+@pytest.mark.parametrize("modem", ["2bits_QPSK.txt", "4bit_16QAM_Gray.txt", "6bits_64QAM_Gray.txt"])
+def test_kmeans_adversarial_ties(data_dir, modem):
+    """Symbols exactly on constellation points, on midpoints between points
+    (distance ties) and at zero, under exact and rotated channels: the
+    squared-norm screening + exact-hypot tie band must reproduce the
+    reference's first-minimum decisions bit for bit."""
+    matrix = "PEG8064regular0.5.txt" if "64QAM" in modem else "PEG2304regular0.5.txt"
+    ctx = ctx_for(data_dir, matrix, modem, False)
+    om = O.Modem(os.path.join(data_dir, modem))
+    pts = om.points.reshape(-1, 2)
+    rng = np.random.default_rng(11)
+    S = ctx.S
+    B = 24
+    y = np.zeros((B, S, 2))
+    for b in range(B):
+        h = [1.0, 0.0] if b % 3 == 0 else ([0.0, 1.0] if b % 3 == 1 else rng.normal(size=2))
+        hc = complex(h[0], h[1])
+        kinds = rng.integers(0, 4, S)
+        i1 = rng.integers(0, len(pts), S)
+        i2 = rng.integers(0, len(pts), S)
+        p1 = pts[i1, 0] + 1j * pts[i1, 1]
+        p2 = pts[i2, 0] + 1j * pts[i2, 1]
+        z = np.where(kinds == 0, p1 * hc, np.where(kinds == 1, (p1 + p2) / 2 * hc,
+                     np.where(kinds == 2, 0.0, p1 * hc + 1e-3 * (rng.normal(size=S) + 1j * rng.normal(size=S)))))
+        y[b, :, 0] = z.real
+        y[b, :, 1] = z.imag
+    hh, h4 = ctx.kmeans(y)
+    for b in range(B):
+        ref = O.kmeans_hhat(y[b], om.points)
+        assert np.array_equal(hh[b], ref, equal_nan=True), b
+
+
 @pytest.mark.parametrize("case", CASES)
 def test_decode_frames_vs_reference_stream(case, data_dir):
     """KmCodec::Decoder on the reference's own frames (regenerated bit-exactly
