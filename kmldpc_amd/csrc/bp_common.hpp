@@ -58,8 +58,10 @@ __device__ __forceinline__ double div1(double n0, double s) {
 }
 
 // Prior values for which the FAST division path is exact (see div2).
+// -0.0 is excluded: with every prior >= +0 no message is ever -0, which makes
+// the x*1.0 / (1,0)-state identities used on the FAST path exact.
 __device__ __forceinline__ bool fast_prior_ok(double q) {
-  return q == 0.0 || q == 1.0 || (q >= 0x1p-40 && q <= 1.0 - 0x1p-40);
+  return (q == 0.0 && __double_as_longlong(q) == 0) || q == 1.0 || (q >= 0x1p-40 && q <= 1.0 - 0x1p-40);
 }
 
 constexpr int kFastMaxColumnDegree = 20;

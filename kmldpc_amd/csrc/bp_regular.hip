@@ -45,47 +45,60 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
                                            const double (&pv)[RV], const int (&crow)[RC], const int (&cbase)[RC],
                                            const int (&ccol)[RC][(DC + 1) / 2], int odd, int &iter_out,
                                            bool &conv_out) {
-  constexpr int H = (DC + 1) / 2;  // edges per half-row (upper half incl. middle for the odd lane)
+  static_assert(DC % 2 == 0, "the lane-pair split assumes an even row degree");
+  constexpr int H = DC / 2;
   int iter = 0;
   bool conv = false;
   for (; iter < a.iter_count; ++iter) {
     // ------------------------------------------------------------ VN phase
+    // The RV columns' chains are interleaved step by step in program order so
+    // their dependent fma / rcp sequences overlap.  On the FAST path the
+    // boundary state beta = (1, 1) is applied as the identity (x * 1.0 == x).
     {
       double c0s[RV][DV];
 #pragma unroll
       for (int r = 0; r < RV; ++r)
 #pragma unroll
         for (int k = 0; k < DV; ++k) c0s[r][k] = slots[vslot[r][k]].x;
+      double a0[RV], a1[RV], al0[RV][DV], al1[RV][DV];
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
-        double a0 = pv[r], a1 = 1.0 - pv[r];
-        double al0[DV], al1[DV];
+        a0[r] = pv[r];
+        a1[r] = 1.0 - pv[r];
+      }
 #pragma unroll
-        for (int k = 0; k < DV; ++k) {
-          al0[k] = a0;
-          al1[k] = a1;
+      for (int k = 0; k < DV; ++k)
+#pragma unroll
+        for (int r = 0; r < RV; ++r) {
+          al0[r][k] = a0[r];
+          al1[r][k] = a1[r];
           const double c0 = c0s[r][k];
-          const double n0 = a0 * c0;
-          const double n1 = a1 * (1.0 - c0);
-          div2<FAST>(n0, n1, n0 + n1, a0, a1);
+          const double n0 = a0[r] * c0;
+          const double n1 = a1[r] * (1.0 - c0);
+          div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r]);
         }
-        cch[vcol[r]] = (a0 > a1) ? 0 : 1;
-        double b0 = 1.0, b1 = 1.0;
 #pragma unroll
-        for (int k = DV - 1; k >= 0; --k) {
-          const double t0 = al0[k] * b0;
-          const double t1 = al1[k] * b1;
+      for (int r = 0; r < RV; ++r) cch[vcol[r]] = (a0[r] > a1[r]) ? 0 : 1;
+      double b0[RV], b1[RV];
+#pragma unroll
+      for (int r = 0; r < RV; ++r) b0[r] = b1[r] = 1.0;
+#pragma unroll
+      for (int k = DV - 1; k >= 0; --k)
+#pragma unroll
+        for (int r = 0; r < RV; ++r) {
+          const bool unit = FAST && k == DV - 1;  // beta = (1, 1)
+          const double t0 = unit ? al0[r][k] : al0[r][k] * b0[r];
+          const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
           double q0, q1;
           div2<FAST>(t0, t1, t0 + t1, q0, q1);
           slots[vslot[r][k]] = make_double2(q0, q1);
           if (k > 0) {
             const double c0 = c0s[r][k];
-            const double n0 = b0 * c0;
-            const double n1 = b1 * (1.0 - c0);
-            div2<FAST>(n0, n1, n0 + n1, b0, b1);
+            const double n0 = unit ? c0 : b0[r] * c0;
+            const double n1 = unit ? (1.0 - c0) : b1[r] * (1.0 - c0);
+            div2<FAST>(n0, n1, n0 + n1, b0[r], b1[r]);
           }
         }
-      }
     }
     __syncthreads();
 
@@ -95,8 +108,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
     for (int r = 0; r < RC; ++r) {
       int p = 0;
 #pragma unroll
-      for (int k = 0; k < H; ++k)
-        if (odd || k < DC / 2) p ^= cch[ccol[r][k]];  // middle edge of an odd row: odd lane only
+      for (int k = 0; k < H; ++k) p ^= cch[ccol[r][k]];
       fail |= p ^ swap_pair_i(p);
     }
     if (!__syncthreads_or(fail)) {
@@ -105,47 +117,65 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
     }
 
     // ------------------------------------------------------------ CN phase
+    // Step s of the even lane advances alpha over edge s, of the odd lane beta
+    // over edge DC-1-s.  From step H on, the pair swaps the chain states and
+    // each lane finishes one c2v per step.  Within a step every message LOAD is
+    // issued before the c2v STOREs (the partner's store of this step hits the
+    // slot the lane is about to read), and LDS executes a wave's operations in
+    // program order.
     {
-      // own-order messages: even lane k = s, odd lane k = DC-1-s
-      double v0[RC][DC], v1[RC][DC];
-#pragma unroll
-      for (int r = 0; r < RC; ++r)
-#pragma unroll
-        for (int s = 0; s < DC; ++s) {
-          const double2 m = slots[cbase[r] + (odd ? DC - 1 - s : s)];
-          v0[r][s] = m.x;
-          v1[r][s] = m.y;
-        }
+      double x0[RC][H], x1[RC][H];  // lower-half chain states, kept for the swap
+      double s0[RC], s1[RC];        // current chain state
 #pragma unroll
       for (int r = 0; r < RC; ++r) {
-        // chain: even lane = alpha (forward), odd lane = beta (backward)
-        double x0[DC], x1[DC];
-        double a0 = 1.0, a1 = 0.0;
+        s0[r] = 1.0;
+        s1[r] = 0.0;
+      }
 #pragma unroll
-        for (int s = 0; s < DC; ++s) {
-          x0[s] = a0;
-          x1[s] = a1;
-          if (SYN || s + 1 < DC) {
-            const double n0 = a0 * v0[r][s] + a1 * v1[r][s];
-            const double n1 = a0 * v1[r][s] + a1 * v0[r][s];
-            div2<FAST>(n0, n1, n0 + n1, a0, a1);
+      for (int st = 0; st < DC; ++st) {
+        const bool advance = SYN || st + 1 < DC;
+        double m0[RC], m1[RC];
+        if (advance) {
+#pragma unroll
+          for (int r = 0; r < RC; ++r) {
+            const double2 m = slots[cbase[r] + (odd ? DC - 1 - st : st)];
+            m0[r] = m.x;
+            m1[r] = m.y;
           }
         }
-        if constexpr (SYN)
-          if (!odd) a.syn[(long long)cw * c.M + crow[r]] = a0;  // alpha past the last edge (:274)
-        // exchange + c2v for the own half: j in [DC/2, DC)
 #pragma unroll
-        for (int j = DC / 2; j < DC; ++j) {
-          const double y0 = swap_pair(x0[j]);
-          const double y1 = swap_pair(x1[j]);
-          const double o0 = x0[DC - 1 - j], o1 = x1[DC - 1 - j];
-          const double t0 = o0 * y0 + o1 * y1;
-          const double t1 = o0 * y1 + o1 * y0;
-          double q = div1<FAST>(t0, t0 + t1);
-          if (q > 1.0 - kSmallestProb) q = 1.0 - kSmallestProb;
-          if (q < kSmallestProb) q = kSmallestProb;
-          slots[cbase[r] + (odd ? j : DC - 1 - j)].x = q;
+        for (int r = 0; r < RC; ++r) {
+          if (st < H) {
+            x0[r][st] = s0[r];
+            x1[r][st] = s1[r];
+          } else {
+            // c2v of edge (odd ? st : DC-1-st) from (own state at DC-1-st, partner state at st)
+            const double y0 = swap_pair(s0[r]);
+            const double y1 = swap_pair(s1[r]);
+            const double o0 = x0[r][DC - 1 - st], o1 = x1[r][DC - 1 - st];
+            const bool unit = FAST && st == DC - 1;  // own state is the boundary (1, 0)
+            const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
+            const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
+            double q = div1<FAST>(t0, t0 + t1);
+            if (q > 1.0 - kSmallestProb) q = 1.0 - kSmallestProb;
+            if (q < kSmallestProb) q = kSmallestProb;
+            slots[cbase[r] + (odd ? st : DC - 1 - st)].x = q;
+          }
         }
+        if (advance) {
+#pragma unroll
+          for (int r = 0; r < RC; ++r) {
+            const bool unit = FAST && st == 0;  // state (1, 0)
+            const double n0 = unit ? m0[r] : s0[r] * m0[r] + s1[r] * m1[r];
+            const double n1 = unit ? m1[r] : s0[r] * m1[r] + s1[r] * m0[r];
+            div2<FAST>(n0, n1, n0 + n1, s0[r], s1[r]);
+          }
+        }
+      }
+      if constexpr (SYN) {
+#pragma unroll
+        for (int r = 0; r < RC; ++r)
+          if (!odd) a.syn[(long long)cw * c.M + crow[r]] = s0[r];  // alpha past the last edge (:274)
       }
     }
     __syncthreads();
@@ -233,8 +263,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
         for (int r = 0; r < RC; ++r) {
           int p = 0;
 #pragma unroll
-          for (int k = 0; k < H; ++k)
-            if (odd || k < DC / 2) p ^= cch[ccol[r][k]];
+          for (int k = 0; k < H; ++k) p ^= cch[ccol[r][k]];
           const int full = p ^ swap_pair_i(p);
           if (!odd) cnt += full;
         }
