@@ -66,4 +66,35 @@ __device__ __forceinline__ bool fast_prior_ok(double q) {
 
 constexpr int kFastMaxColumnDegree = 20;
 
+// ProbClip of a c2v message (binaryldpccodec.cc:260-263).  On the FAST path the
+// value is finite (no NaN), where min(max(q, lo), hi) is the same two tests.
+template <bool FAST>
+__device__ __forceinline__ double clip_c2v(double q) {
+  if constexpr (FAST) {
+    return fmin(fmax(q, kSmallestProb), 1.0 - kSmallestProb);
+  } else {
+    if (q > 1.0 - kSmallestProb) q = 1.0 - kSmallestProb;
+    if (q < kSmallestProb) q = kSmallestProb;
+    return q;
+  }
+}
+
+// Hard decision of a column from the un-normalised posterior (n0, n1):
+// the reference compares RN(n0/s) > RN(n1/s) with s = n0 + n1
+// (binaryldpccodec.cc:186-194).  When n0 and n1 differ by more than 2^-48
+// relative, the rounded quotients are ordered like n0, n1 (RN is monotone and
+// the gap exceeds an ulp); only then is the division skipped (FAST path, all
+// values finite and >= +0).
+template <bool FAST>
+__device__ __forceinline__ int hard_decision(double n0, double n1) {
+  if constexpr (FAST) {
+    const double g = 1.0 + 0x1p-48;
+    if (n0 > n1 * g) return 0;
+    if (n1 > n0 * g) return 1;
+  }
+  double a0, a1;
+  div2<FAST>(n0, n1, n0 + n1, a0, a1);
+  return (a0 > a1) ? 0 : 1;
+}
+
 }  // namespace kml

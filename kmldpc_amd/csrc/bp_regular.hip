@@ -21,6 +21,12 @@
 //     the CN phase has exactly as many lanes busy as the VN phase.
 //   * the early-stop parity check XORs the two half-rows through the same DPP
 //     swap.
+//   * LDS placement (layout.hpp): the columns' lane assignment is annealed on
+//     the host against the VN phase's bank conflicts, the hard decisions are
+//     stored by lane position (contiguous byte stores), and a c2v message goes
+//     to the lower or upper half of its slot by bit 2 of the row's CN position,
+//     so that a 16-lane ds_write_b64 group of the CN phase hits 16 distinct
+//     bank pairs.  The VN phase reads it at the planned byte offset.
 #include "bp_common.hpp"
 #include "kernels.hpp"
 
@@ -40,11 +46,13 @@ __device__ __forceinline__ double swap_pair(double x) {
 __device__ __forceinline__ int swap_pair_i(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }
 
 template <int T, int RV, int RC, int DV, int DC, bool SYN, bool FAST>
-__device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, int cw, double2 *slots,
-                                           unsigned char *cch, const int (&vcol)[RV], const int (&vslot)[RV][DV],
-                                           const double (&pv)[RV], const int (&crow)[RC], const int (&cbase)[RC],
-                                           const int (&ccol)[RC][(DC + 1) / 2], int odd, int &iter_out,
+__device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, int cw, unsigned char *smem,
+                                           unsigned char *cch, const int (&vaddr)[RV][DV], const double (&pv)[RV],
+                                           const int (&crow)[RC], const int (&cbase)[RC],
+                                           const int (&ccol)[RC][(DC + 1) / 2], int odd, int chalf, int &iter_out,
                                            bool &conv_out) {
+  const int tid = threadIdx.x;
+  double2 *slots = reinterpret_cast<double2 *>(smem);
   static_assert(DC % 2 == 0, "the lane-pair split assumes an even row degree");
   constexpr int H = DC / 2;
   int iter = 0;
@@ -59,7 +67,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
 #pragma unroll
       for (int r = 0; r < RV; ++r)
 #pragma unroll
-        for (int k = 0; k < DV; ++k) c0s[r][k] = slots[vslot[r][k]].x;
+        for (int k = 0; k < DV; ++k) c0s[r][k] = *reinterpret_cast<const double *>(smem + vaddr[r][k]);
       double a0[RV], a1[RV], al0[RV][DV], al1[RV][DV];
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
@@ -75,10 +83,11 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
           const double c0 = c0s[r][k];
           const double n0 = a0[r] * c0;
           const double n1 = a1[r] * (1.0 - c0);
-          div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r]);
+          if (k + 1 < DV)
+            div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r]);
+          else  // the posterior only feeds the hard decision
+            cch[r * T + tid] = (unsigned char)hard_decision<FAST>(n0, n1);
         }
-#pragma unroll
-      for (int r = 0; r < RV; ++r) cch[vcol[r]] = (a0[r] > a1[r]) ? 0 : 1;
       double b0[RV], b1[RV];
 #pragma unroll
       for (int r = 0; r < RV; ++r) b0[r] = b1[r] = 1.0;
@@ -91,7 +100,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
           const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
           double q0, q1;
           div2<FAST>(t0, t1, t0 + t1, q0, q1);
-          slots[vslot[r][k]] = make_double2(q0, q1);
+          *reinterpret_cast<double2 *>(smem + (vaddr[r][k] & ~8)) = make_double2(q0, q1);
           if (k > 0) {
             const double c0 = c0s[r][k];
             const double n0 = unit ? c0 : b0[r] * c0;
@@ -156,10 +165,8 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
             const bool unit = FAST && st == DC - 1;  // own state is the boundary (1, 0)
             const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
             const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
-            double q = div1<FAST>(t0, t0 + t1);
-            if (q > 1.0 - kSmallestProb) q = 1.0 - kSmallestProb;
-            if (q < kSmallestProb) q = kSmallestProb;
-            slots[cbase[r] + (odd ? st : DC - 1 - st)].x = q;
+            *reinterpret_cast<double *>(smem + (cbase[r] + (odd ? st : DC - 1 - st)) * 16 + chalf) =
+                clip_c2v<FAST>(div1<FAST>(t0, t0 + t1));
           }
         }
         if (advance) {
@@ -194,15 +201,16 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
   int *red = reinterpret_cast<int *>(smem + (size_t)c.E * 16);
   unsigned char *cch = smem + (size_t)c.E * 16 + kRedBytes;
 
-  int vcol[RV], vslot[RV][DV];
+  int vcol[RV], vaddr[RV][DV];
 #pragma unroll
   for (int r = 0; r < RV; ++r) {
     const int v = c.vn_order[r * T + tid];
     const int b = c.col_ptr[v];
     vcol[r] = v;
 #pragma unroll
-    for (int k = 0; k < DV; ++k) vslot[r][k] = c.col_slot[b + k];
+    for (int k = 0; k < DV; ++k) vaddr[r][k] = c.reg_c2v[b + k];
   }
+  const int chalf = ((tid >> 3) & 1) * 8;  // bit 2 of the CN position (tid >> 1)
   int crow[RC], cbase[RC], ccol[RC][H];
 #pragma unroll
   for (int r = 0; r < RC; ++r) {
@@ -212,7 +220,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
 #pragma unroll
     for (int k = 0; k < H; ++k) {  // parity columns: even lane edges [0, DC/2), odd lane [DC/2, DC)
       const int e = odd ? DC / 2 + k : k;
-      ccol[r][k] = c.row_col[cbase[r] + (e < DC ? e : DC - 1)];
+      ccol[r][k] = c.reg_pos[c.row_col[cbase[r] + (e < DC ? e : DC - 1)]];
     }
   }
 
@@ -236,26 +244,26 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
       pv[r] = (vcol[r] >= c.punct) ? p0[vcol[r] - c.punct] : 0.5;
       ok = ok && fast_prior_ok(pv[r]);
     }
-    for (int e = tid; e < c.E; e += T) slots[e].x = 0.5;  // InitMsg
+    for (int e = tid; e < c.E; e += T) slots[e] = make_double2(0.5, 0.5);  // InitMsg (either c2v half)
     const bool fast = __syncthreads_and(ok ? 1 : 0) && fast_allowed;
 
     int iter = 0;
     bool conv = false;
     if (fast)
-      decode_reg<T, RV, RC, DV, DC, SYN, true>(c, a, cw, slots, cch, vcol, vslot, pv, crow, cbase, ccol, odd, iter,
+      decode_reg<T, RV, RC, DV, DC, SYN, true>(c, a, cw, smem, cch, vaddr, pv, crow, cbase, ccol, odd, chalf, iter,
                                               conv);
     else
-      decode_reg<T, RV, RC, DV, DC, SYN, false>(c, a, cw, slots, cch, vcol, vslot, pv, crow, cbase, ccol, odd, iter,
+      decode_reg<T, RV, RC, DV, DC, SYN, false>(c, a, cw, smem, cch, vaddr, pv, crow, cbase, ccol, odd, chalf, iter,
                                                conv);
 
     if (a.iter_count > 0) {
       if (a.uu_hat) {
         uint8_t *u = a.uu_hat + (long long)cw * c.K;
-        for (int i = tid; i < c.K; i += T) u[i] = cch[i + c.info_off];
+        for (int i = tid; i < c.K; i += T) u[i] = cch[c.reg_pos[i + c.info_off]];
       }
       if (a.cc_hat) {
         uint8_t *o = a.cc_hat + (long long)cw * c.N;
-        for (int v = tid; v < c.N; v += T) o[v] = cch[v];
+        for (int v = tid; v < c.N; v += T) o[v] = cch[c.reg_pos[v]];
       }
       if (a.parity_cnt) {
         int cnt = 0;
@@ -276,7 +284,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
           uint64_t word = 0;
           const int base = w * 64;
           const int nb = min(64, c.K - base);
-          for (int j = 0; j < nb; ++j) word |= (uint64_t)cch[c.info_off + base + j] << j;
+          for (int j = 0; j < nb; ++j) word |= (uint64_t)cch[c.reg_pos[c.info_off + base + j]] << j;
           errs += __popcll(word ^ ref[w]);
         }
         if (errs) atomicAdd(&red[1], errs);
@@ -322,13 +330,18 @@ hipError_t launch_reg_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int 
 
 }  // namespace
 
-hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s) {
-  if (!c.regular || (long long)c.E * 16 + kRedBytes + c.N > 160 * 1024) return hipErrorNotSupported;
-  const int fast = c.dv_max <= kFastMaxColumnDegree ? 1 : 0;
+int bp_regular_threads(int N, int M, int E, int dv_max, int dc_max, int regular) {
+  if (!regular || (long long)E * 16 + kRedBytes + N > 160 * 1024) return 0;
   // PEG2304-class: dv 3, dc 6, N = 3*768, 2M = 3*768
-  if (c.dv_max == 3 && c.dc_max == 6 && c.N == 3 * 768 && 2 * c.M == 3 * 768)
-    return a.syn ? launch_reg_t<768, 3, 3, 3, 6, true>(c, a, s, fast) : launch_reg_t<768, 3, 3, 3, 6, false>(c, a, s, fast);
-  return hipErrorNotSupported;
+  if (dv_max == 3 && dc_max == 6 && N == 3 * 768 && 2 * M == 3 * 768) return 768;
+  return 0;
+}
+
+hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s) {
+  if (!c.reg_c2v || bp_regular_threads(c.N, c.M, c.E, c.dv_max, c.dc_max, c.regular) != 768)
+    return hipErrorNotSupported;
+  const int fast = c.dv_max <= kFastMaxColumnDegree ? 1 : 0;
+  return a.syn ? launch_reg_t<768, 3, 3, 3, 6, true>(c, a, s, fast) : launch_reg_t<768, 3, 3, 3, 6, false>(c, a, s, fast);
 }
 
 }  // namespace kml

@@ -13,6 +13,7 @@
 #include "code.hpp"
 #include "config.hpp"
 #include "kernels.hpp"
+#include "layout.hpp"
 #include "modem.hpp"
 
 namespace {
@@ -116,10 +117,21 @@ int upload_code(kml_ctx *c) {
   reserve(L.row_ptr.size() * 4);
   reserve(L.row_col.size() * 4);
   reserve(L.col_ptr.size() * 4);
+  int regular = 1;
+  for (int j = 0; j < L.N; j++)
+    if (L.col_ptr[j + 1] - L.col_ptr[j] != L.dv_max) regular = 0;
+  for (int i = 0; i < L.M; i++)
+    if (L.row_ptr[i + 1] - L.row_ptr[i] != L.dc_max) regular = 0;
+  const int reg_T = kml::bp_regular_threads(L.N, L.M, L.E, L.dv_max, L.dc_max, regular);
+  kml::RegularLayout plan;
+  if (reg_T > 0) kml::plan_regular_layout(L, reg_T, plan);
+  const std::vector<int32_t> &vn_order = reg_T > 0 ? plan.order : L.vn_order;
   reserve(L.col_slot.size() * 4);
-  reserve(L.vn_order.size() * 4);
+  reserve(vn_order.size() * 4);
   reserve(L.cn_order.size() * 4);
   reserve(std::max<size_t>(L.enc_info.size(), 1) * 8);
+  reserve(plan.c2v_addr.size() * 4);
+  reserve(plan.pos.size() * 4);
   HIPCHK(c, c->d_graph.ensure(bytes), "hipMalloc(graph)");
   std::vector<unsigned char> host(bytes, 0);
   auto put = [&](int i, const void *src, size_t n) {
@@ -129,9 +141,11 @@ int upload_code(kml_ctx *c) {
   put(1, L.row_col.data(), L.row_col.size() * 4);
   put(2, L.col_ptr.data(), L.col_ptr.size() * 4);
   put(3, L.col_slot.data(), L.col_slot.size() * 4);
-  put(4, L.vn_order.data(), L.vn_order.size() * 4);
+  put(4, vn_order.data(), vn_order.size() * 4);
   put(5, L.cn_order.data(), L.cn_order.size() * 4);
   put(6, L.enc_info.data(), L.enc_info.size() * 8);
+  put(7, plan.c2v_addr.data(), plan.c2v_addr.size() * 4);
+  put(8, plan.pos.data(), plan.pos.size() * 4);
   HIPCHK(c, hipMemcpy(c->d_graph.p, host.data(), bytes, hipMemcpyHostToDevice), "upload graph");
   unsigned char *base = c->d_graph.as<unsigned char>();
   kml::DevCode &d = c->dc;
@@ -142,6 +156,8 @@ int upload_code(kml_ctx *c) {
   d.vn_order = reinterpret_cast<const int32_t *>(base + off[4]);
   d.cn_order = reinterpret_cast<const int32_t *>(base + off[5]);
   d.enc_info = reinterpret_cast<const uint64_t *>(base + off[6]);
+  d.reg_c2v = reg_T > 0 ? reinterpret_cast<const int32_t *>(base + off[7]) : nullptr;
+  d.reg_pos = reg_T > 0 ? reinterpret_cast<const int32_t *>(base + off[8]) : nullptr;
   d.M = L.M;
   d.N = L.N;
   d.E = L.E;
@@ -155,11 +171,7 @@ int upload_code(kml_ctx *c) {
   d.dc_max = L.dc_max;
   d.is5g = L.is5g ? 1 : 0;
   d.active = L.active ? 1 : 0;
-  d.regular = 1;
-  for (int j = 0; j < L.N; j++)
-    if (L.col_ptr[j + 1] - L.col_ptr[j] != L.dv_max) d.regular = 0;
-  for (int i = 0; i < L.M; i++)
-    if (L.row_ptr[i + 1] - L.row_ptr[i] != L.dc_max) d.regular = 0;
+  d.regular = regular;
 
   HIPCHK(c, c->d_cons.ensure(sizeof(double) * (c->modem.pts.size() + 8)), "hipMalloc(cons)");
   kml::rotation_factors(c->rot);

@@ -22,6 +22,10 @@ struct DevCode {
   const uint64_t *enc_info;
   int M, N, E, K, cc_len, punct, info_off, chk, Kw, dv_max, dc_max, is5g, active;
   int regular;  // every column has degree dv_max and every row dc_max
+  // LDS placement plan of bp_regular.hip (layout.hpp); null when the code does
+  // not take that kernel.  vn_order then holds the planned column order.
+  const int32_t *reg_c2v;  // aligned with col_slot: byte offset of the c2v message
+  const int32_t *reg_pos;  // column -> position (index into the kernel's hard-decision bytes)
 };
 
 // Counter block in device memory (uint64):
@@ -60,6 +64,9 @@ struct BpLaunch {
 // fits it, else to the generic kernel (bp.hip).
 hipError_t launch_bp_static(const DevCode &c, const BpLaunch &a, hipStream_t s);
 hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s);
+// Threads per workgroup of the regular kernel for this code shape, 0 if it does
+// not apply (host-side; decides whether upload_code builds the LDS plan).
+int bp_regular_threads(int N, int M, int E, int dv_max, int dc_max, int regular);
 hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const char **err);
 // Workspace the BP launcher needs in global-slot mode (double2 elements).
 long long bp_gslots_needed(const DevCode &c);
