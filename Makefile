@@ -1,22 +1,27 @@
 # Top-level build: the product library (gfx950 HIP) and the test oracle.
 #
-#   make            -> kmldpc_amd/libkmldpc_amd.so, kmldpc_amd/bin/kmldpc_gpu, oracle/*
-#   make lib        -> product library only
+#   make            -> kmldpc_amd/libkmldpc_amd.so, kmldpc_amd/bin/kmldpc_sim, oracle/*
+#   make lib        -> product library + the kmldpc_sim driver executable
 #   make oracle     -> oracle/liboracle.so, oracle/cpu_baseline (+ oracle/_ref when /root/reference exists)
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result -Wno-unused-value
 CSRC     := kmldpc_amd/csrc
 OBJDIR   := build/obj
-CPP_SRCS := config code modem layout capi
+CPP_SRCS := config code modem layout capi simulate
 HIP_SRCS := bp bp_static bp_regular demap kmeans framegen
 OBJS     := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(CPP_SRCS) $(HIP_SRCS)))
 HDRS     := $(wildcard $(CSRC)/*.hpp) include/kmldpc_amd.h
 LIB      := kmldpc_amd/libkmldpc_amd.so
+SIM      := kmldpc_amd/bin/kmldpc_sim
 
 all: lib oracle
 
-lib: $(LIB)
+lib: $(LIB) $(SIM)
+
+$(SIM): $(CSRC)/sim_main.cpp include/kmldpc_amd.h $(LIB)
+	@mkdir -p kmldpc_amd/bin
+	g++ -O2 -std=c++17 -Wall -o $@ $< -Lkmldpc_amd -lkmldpc_amd -Wl,-rpath,'$$ORIGIN/..'
 
 $(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -33,7 +38,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(SIM)
 	$(MAKE) -C oracle clean
 
 .PHONY: all lib oracle clean

@@ -26,7 +26,9 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-import kmldpc_amd as K  # noqa: E402  (load the HIP library before torch)
+import kmldpc_amd as K  # noqa: E402
+
+K.lib()  # load the HIP library (and its ROCm runtime) before torch
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 dense peak (vector = matrix rate, AMD spec)

@@ -134,6 +134,58 @@ int kml_sim_generate(kml_ctx *ctx, double snr, uint64_t seed, uint64_t first_cw,
  * kml_sync to wait. */
 int kml_sim_decode(kml_ctx *ctx, double snr, int blind, uint64_t *counters, int sync);
 int kml_sync(kml_ctx *ctx);
+/* Synchronous form with the per-codeword view the simulator's stop rule needs:
+ * cw_err[B] (may be NULL) = error bits of each resident codeword, metrics[B][4]
+ * (may be NULL) = the candidate metrics.  histogram != 0 runs
+ * KmCodec::GetHistogramData instead of Decoder (simulator.cc:154-162): metrics
+ * only, no final decode, and the error count then sees the uu_hat the last
+ * metric decode left (5G metric) or all-zero decisions (hard PEG metric, whose
+ * reference buffer is uninitialised).  counters[8] as kml_sim_decode. */
+int kml_sim_decode_ex(kml_ctx *ctx, double snr, int blind, int histogram, int32_t *cw_err, double *metrics,
+                      uint64_t *counters);
+
+/* --- simulator driver (Simulator::Simulate / run / run_blocks) ------------ */
+/* The parsed config.toml: f[3] = {minimum_snr, maximum_snr, step_snr};
+ * n[10] = {maximum_error_number, maximum_block_number, thread_block_number,
+ * true_h_arg, 5gldpc, metric_type, metric_iter, histogram.enable, max_iter,
+ * active}. */
+int kml_run_config(const kml_ctx *ctx, double *f, int64_t *n);
+
+/* In-place sum of n counters over all ranks (RCCL / gloo / MPI in the caller). */
+typedef int (*kml_allreduce_fn)(uint64_t *vals, int n, void *user);
+/* Decode `count` frames with global codeword indices [first_cw, first_cw+count):
+ * cw_err[count] error bits per codeword, metrics[count][4] (histogram mode). */
+typedef int (*kml_batch_fn)(uint64_t first_cw, int count, int32_t *cw_err, double *metrics, void *user);
+/* Progress: counters {err_bit, err_blk, tot_bit, tot_blk} (SourceSink::PrintResult). */
+typedef void (*kml_report_fn)(const uint64_t *counters, void *user);
+
+typedef struct {
+  double snr;
+  int rank, world;       /* this process's shard of the codeword index space */
+  int batch;             /* codewords per rank per round */
+  uint64_t max_blocks;   /* maximum_block_number */
+  uint64_t max_err;      /* maximum_error_number */
+  int K;                 /* info bits per codeword (tot_bit += K) */
+  int ncand;             /* histogram: metrics per codeword (1 known-H, 4 blind) */
+  const char *hist_path; /* histogram output file of this rank, NULL = none */
+  int report_every;      /* PrintResult period in codewords (reference: 100) */
+} kml_point_cfg;
+
+/* One SNR point of Simulator::run with the stop rule of run_blocks
+ * (simulator.cc:117): codewords are taken in global index order until
+ * maximum_block_number are counted or maximum_error_number block errors
+ * reached, exactly as a single sequential stream would, whatever world and
+ * batch are.  Rank r decodes indices [t*world*batch + r*batch, ...) of round t;
+ * per round the ranks exchange world + 4 counters through `reduce` (no
+ * per-codeword data moves between ranks).  counters[4] = the point's totals
+ * {err_bit, err_blk, tot_bit, tot_blk}. */
+int kml_sweep_point(const kml_point_cfg *cfg, kml_batch_fn decode, void *decode_user, kml_allreduce_fn reduce,
+                    void *reduce_user, kml_report_fn report, void *report_user, uint64_t *counters);
+/* kml_sweep_point with the context's GPU frame generator (Philox keyed by
+ * seed and global codeword index) and receive path ([decoder] true_h_arg,
+ * [histogram] enable from the config). */
+int kml_sim_point(kml_ctx *ctx, const kml_point_cfg *cfg, uint64_t seed, kml_allreduce_fn reduce, void *reduce_user,
+                  kml_report_fn report, void *report_user, uint64_t *counters);
 /* Copy the resident frames out (for checks): uu[B][K] bytes, y[B][S][2], h[B][2]. */
 int kml_sim_frames(kml_ctx *ctx, uint8_t *uu, double *y, double *h);
 

@@ -13,6 +13,9 @@ raises.  The class names mirror the reference's C++ interface
     Context.decode_frames      KmCodec::Decoder                          src/kmcodec.cc:54-72
     Context.count_errors       lab::SourceSink::CntErr                   lib/lab/src/sourcesink.cc:29-47
     Context.sim_generate/decode  one SNR point of Simulator::run_blocks   src/simulator.cc:112-168
+    Context.sim_point          Simulator::run (stop rule, rank sharding) src/simulator.cc:72-110
+    sweep_point                the same driver logic with caller-supplied decode / all-reduce
+    kmldpc_amd.simulate        Simulator::Simulate + main (SNR sweep, console / log output)
 """
 import ctypes as C
 import os
@@ -31,6 +34,20 @@ DIM_NAMES = ["M", "Ncol", "K", "cc_len", "Z", "E", "chk", "max_iter", "bits", "K
 
 class KmlError(RuntimeError):
     pass
+
+
+# kml_point_cfg and the driver callbacks (include/kmldpc_amd.h)
+class PointCfg(C.Structure):
+    _fields_ = [("snr", C.c_double), ("rank", C.c_int), ("world", C.c_int), ("batch", C.c_int),
+                ("max_blocks", C.c_uint64), ("max_err", C.c_uint64), ("K", C.c_int), ("ncand", C.c_int),
+                ("hist_path", C.c_char_p), ("report_every", C.c_int)]
+
+
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_uint64), C.c_int, C.c_void_p)
+BATCH_FN = C.CFUNCTYPE(C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_double), C.c_void_p)
+REPORT_FN = C.CFUNCTYPE(None, C.POINTER(C.c_uint64), C.c_void_p)
+RUN_CONFIG_KEYS = ["maximum_error_number", "maximum_block_number", "thread_block_number", "true_h_arg", "5gldpc",
+                   "metric_type", "metric_iter", "histogram", "max_iter", "active"]
 
 
 _lib = None
@@ -72,6 +89,10 @@ def lib():
         "kml_prof_read_flops": (I, [P, C.c_char_p, P]),
         "kml_math_probe": (I, [P, P, I, P]),
         "kml_div_probe": (I, [P, P, I, P]),
+        "kml_sim_decode_ex": (I, [P, D, I, I, P, P, P]),
+        "kml_run_config": (I, [P, P, P]),
+        "kml_sweep_point": (I, [C.POINTER(PointCfg), BATCH_FN, P, ALLREDUCE_FN, P, REPORT_FN, P, P]),
+        "kml_sim_point": (I, [P, C.POINTER(PointCfg), C.c_uint64, ALLREDUCE_FN, P, REPORT_FN, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -127,6 +148,7 @@ class Context:
         for k, v in self.dims.items():
             setattr(self, k, v)
         self.device = device
+        self._sim_B = 0
 
     def close(self):
         if getattr(self, "_h", None):
@@ -232,6 +254,7 @@ class Context:
 
     def sim_generate(self, snr, B, seed=17, first_cw=0):
         self._chk(lib().kml_sim_generate(self._h, float(snr), int(seed), int(first_cw), int(B)), "kml_sim_generate")
+        self._sim_B = int(B)
 
     def sim_decode(self, snr, blind=False, sync=True):
         if not sync:
@@ -244,6 +267,36 @@ class Context:
 
     def sync(self):
         self._chk(lib().kml_sync(self._h), "kml_sync")
+
+    def sim_decode_ex(self, snr, blind=False, histogram=False):
+        """Synchronous sim decode with per-codeword error bits and metrics."""
+        B = self._sim_B
+        err = np.zeros(B, np.int32)
+        met = np.zeros((B, 4))
+        cnt = np.zeros(8, np.uint64)
+        self._chk(lib().kml_sim_decode_ex(self._h, float(snr), int(blind), int(histogram), _p(err), _p(met), _p(cnt)),
+                  "kml_sim_decode_ex")
+        return err, met, dict(zip(["err_bit", "err_blk", "tot_bit", "tot_blk", "vn_phases", "cn_phases",
+                                   "converged"], [int(x) for x in cnt[:7]]))
+
+    def run_config(self):
+        """The parsed config.toml ([range], [decoder], [xcodec], [histogram], [ldpc])."""
+        f = np.zeros(3)
+        n = np.zeros(10, np.int64)
+        self._chk(lib().kml_run_config(self._h, _p(f), _p(n)), "kml_run_config")
+        d = dict(minimum_snr=float(f[0]), maximum_snr=float(f[1]), step_snr=float(f[2]))
+        d.update({k: int(v) for k, v in zip(RUN_CONFIG_KEYS, n)})
+        return d
+
+    def sim_point(self, snr, seed, *, rank=0, world=1, batch=32768, max_blocks, max_err, hist_path=None,
+                  reduce=None, report=None, report_every=100):
+        """One SNR point of Simulator::run on this GPU (kml_sim_point); see sweep_point for reduce/report."""
+        cfg = point_cfg(snr, rank, world, batch, max_blocks, max_err, self.K, 4, hist_path, report_every)
+        cnt = np.zeros(4, np.uint64)
+        rf, pf = _reduce_cb(reduce), _report_cb(report)
+        self._chk(lib().kml_sim_point(self._h, C.byref(cfg), int(seed), rf, None, pf, None, _p(cnt)),
+                  "kml_sim_point")
+        return dict(zip(["err_bit", "err_blk", "tot_bit", "tot_blk"], [int(x) for x in cnt]))
 
     def sim_frames(self, B):
         uu = np.zeros((B, self.K), np.uint8)
@@ -278,6 +331,70 @@ class Context:
         out = np.zeros_like(x)
         self._chk(lib().kml_math_probe(self._h, _p(x), x.shape[0], _p(out)), "kml_math_probe")
         return out
+
+
+# ---------------------------------------------------------------------------
+# Simulator driver host logic (kml_sweep_point): stop rule + rank sharding.
+
+def point_cfg(snr, rank, world, batch, max_blocks, max_err, K, ncand=4, hist_path=None, report_every=100):
+    return PointCfg(float(snr), int(rank), int(world), int(batch), int(max_blocks), int(max_err), int(K),
+                    int(ncand), os.fsencode(hist_path) if hist_path else None, int(report_every))
+
+
+def _reduce_cb(fn):
+    """fn(np.ndarray[uint64]) -> summed array over ranks (in place or returned)."""
+    if fn is None:
+        return ALLREDUCE_FN()
+
+    def cb(vals, n, _user):
+        try:
+            a = np.ctypeslib.as_array(vals, shape=(n,))
+            r = fn(a.copy())
+            a[:] = np.asarray(r if r is not None else a, dtype=np.uint64)
+            return 0
+        except Exception:  # never let a Python exception unwind through C
+            import traceback
+            traceback.print_exc()
+            return -1
+    return ALLREDUCE_FN(cb)
+
+
+def _report_cb(fn):
+    if fn is None:
+        return REPORT_FN()
+
+    def cb(c, _user):
+        try:
+            fn([int(c[i]) for i in range(4)])
+        except Exception:
+            import traceback
+            traceback.print_exc()
+    return REPORT_FN(cb)
+
+
+def sweep_point(snr, decode, *, K, batch, max_blocks, max_err, rank=0, world=1, reduce=None, report=None,
+                hist_path=None, ncand=4, report_every=100):
+    """kml_sweep_point with Python callbacks: decode(first_cw, count) ->
+    (err[count] int, metrics[count][4] or None); reduce(np.uint64 array) -> sum
+    over ranks; report([err_bit, err_blk, tot_bit, tot_blk])."""
+    def dcb(first, count, err, met, _user):
+        try:
+            e, m = decode(int(first), int(count))
+            np.ctypeslib.as_array(err, shape=(count,))[:] = np.asarray(e, np.int32)
+            if met and m is not None:
+                np.ctypeslib.as_array(met, shape=(count, 4))[:] = np.asarray(m, np.float64)
+            return 0
+        except Exception:
+            import traceback
+            traceback.print_exc()
+            return -1
+    cfg = point_cfg(snr, rank, world, batch, max_blocks, max_err, K, ncand, hist_path, report_every)
+    cnt = np.zeros(4, np.uint64)
+    bf, rf, pf = BATCH_FN(dcb), _reduce_cb(reduce), _report_cb(report)
+    r = lib().kml_sweep_point(C.byref(cfg), bf, None, rf, None, pf, None, _p(cnt))
+    if r != 0:
+        raise KmlError(f"kml_sweep_point failed (code {r})")
+    return dict(zip(["err_bit", "err_blk", "tot_bit", "tot_blk"], [int(x) for x in cnt]))
 
 
 # ---------------------------------------------------------------------------

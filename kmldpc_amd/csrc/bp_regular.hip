@@ -294,6 +294,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
     if (tid == 0) {
       if (a.ret) a.ret[cw] = iter + (iter < a.max_iter);
       if (a.parity_cnt) a.parity_cnt[cw] = red[0];
+      if (a.cw_err && a.ref_bits) a.cw_err[cw] = a.iter_count > 0 ? red[1] : 0;
       if (a.counters) {
         const unsigned long long vn = conv ? (unsigned long long)iter + 1 : (unsigned long long)iter;
         atomicAdd(&a.counters[CNT_VN_PHASES], vn);

@@ -75,7 +75,7 @@ struct kml_ctx {
   DBuf d_queue, d_gslots;
   long long gslots_cap = 0;
   // workspaces
-  DBuf w_y, w_h, w_h4, w_hhat, w_p0, w_uu, w_uh, w_ret, w_cch, w_syn, w_sel, w_met, w_pc, w_cnt, w_km;
+  DBuf w_y, w_h, w_h4, w_hhat, w_p0, w_uu, w_uh, w_uh4, w_ret, w_cch, w_syn, w_sel, w_met, w_pc, w_cnt, w_km, w_cwerr;
   // resident simulation frames
   DBuf s_uu, s_cc, s_y, s_h;
   int sim_B = 0;
@@ -345,49 +345,77 @@ int need_gpu(kml_ctx *c) {
     if (_r != KML_OK) return _r; \
   } while (0)
 
-// Receive path shared by kml_decode_frames and kml_sim_decode: y/h are
-// device pointers.  Produces p0 selection + BP.
-int receive(kml_ctx *c, const double2 *y, const double2 *true_h, double snr, int B, uint8_t *d_uh, int32_t *d_chosen,
-            double *d_met, int32_t *d_ret, double2 *d_hhat, const uint64_t *ref_bits, int &bp_slot) {
+// Receive path shared by kml_decode_frames, kml_sim_decode and
+// kml_sim_histogram.  All pointers are device pointers.
+struct RecvIO {
+  const double2 *y = nullptr;
+  const double2 *true_h = nullptr;  // known channel (simulator.cc:132-133); NULL = blind
+  uint8_t *uh = nullptr;            // uu_hat[B][K] (NULL: not kept)
+  int32_t *chosen = nullptr;        // [B]
+  double *met = nullptr;            // [B][4]
+  int32_t *ret = nullptr;           // [B]
+  double2 *hhat = nullptr;          // [B] k-means h_hat
+  const uint64_t *ref_bits = nullptr;  // packed source bits for CntErr
+  int32_t *cw_err = nullptr;           // [B] error bits per codeword
+  // GetHistogramData instead of Decoder (simulator.cc:154-162): candidate
+  // metrics only, no final decode; CntErr then sees the uu_hat left by the last
+  // candidate's metric decode (5G metric), or all zeros for the hard PEG metric
+  // (the reference's uu_hat buffer is uninitialised there).
+  bool histogram = false;
+};
+
+int receive(kml_ctx *c, const RecvIO &io, double snr, int B, int &bp_slot) {
   double var, sigma, ns;
   kml::channel_constants(snr, var, sigma, ns);
   const int S = c->code.cc_len / c->modem.bits;
   const double *cons = c->d_cons.as<double>();
   const double *rot = cons + c->modem.pts.size();
   const size_t cc = (size_t)c->code.cc_len;
+  const int K = c->code.K;
   kml::BpLaunch a;
   a.B = B;
   a.iter_count = c->rc.max_iter;
   a.max_iter = c->rc.max_iter;
-  a.uu_hat = d_uh;
-  a.ret = d_ret;
-  a.ref_bits = ref_bits;
-  if (true_h) {  // known channel (simulator.cc:132-133)
+  a.uu_hat = io.uh;
+  a.ret = io.ret;
+  a.ref_bits = io.ref_bits;
+  a.cw_err = io.cw_err;
+  if (io.true_h && !io.histogram) {  // known channel: one demap + BP
     HIPCHK(c, c->w_p0.ensure(sizeof(double) * cc * B), "hipMalloc(p0)");
     Timer t(c, "demap", -1, (double)B * S * (16.0 + 8.0 * c->modem.bits));
-    HIPCHK(c, kml::launch_demap(c->modem.bits, cons, y, S, 1, true_h, 1, nullptr, var, B, c->w_p0.as<double>(), c->stream),
+    HIPCHK(c, kml::launch_demap(c->modem.bits, cons, io.y, S, 1, io.true_h, 1, nullptr, var, B, c->w_p0.as<double>(),
+                                c->stream),
            "demap");
     t.stop();
     a.p0 = c->w_p0.as<double>();
     a.p0_stride = (long long)cc;
     return run_bp(c, a, bp_slot);
   }
-  // blind: k-means (simulator.cc:136-148)
-  HIPCHK(c, c->w_h4.ensure(sizeof(double2) * 4 * B), "hipMalloc(h4)");
-  double2 *hh = d_hhat;
-  if (!hh) {
-    HIPCHK(c, c->w_hhat.ensure(sizeof(double2) * B), "hipMalloc(hhat)");
-    hh = c->w_hhat.as<double2>();
-  }
-  {
+  // candidate channel estimates: the true h (histogram on the known-H path) or
+  // k-means + 4 rotations (simulator.cc:136-148)
+  const double2 *hc;
+  int nc;
+  if (io.true_h) {
+    hc = io.true_h;
+    nc = 1;
+  } else {
+    HIPCHK(c, c->w_h4.ensure(sizeof(double2) * 4 * B), "hipMalloc(h4)");
+    double2 *hh = io.hhat;
+    if (!hh) {
+      HIPCHK(c, c->w_hhat.ensure(sizeof(double2) * B), "hipMalloc(hhat)");
+      hh = c->w_hhat.as<double2>();
+    }
     HIPCHK(c, c->w_km.ensure(kml::kmeans_workspace_bytes(S, B)), "hipMalloc(kmeans)");
     Timer t(c, "kmeans", -1, (double)B * S * 16.0);
-    HIPCHK(c, kml::launch_kmeans(c->modem.Kc, cons, rot, y, S, 20, B, hh, c->w_h4.as<double2>(), c->w_km.p, c->stream),
+    HIPCHK(c, kml::launch_kmeans(c->modem.Kc, cons, rot, io.y, S, 20, B, hh, c->w_h4.as<double2>(), c->w_km.p,
+                                 c->stream),
            "kmeans");
     t.stop();
+    hc = c->w_h4.as<double2>();
+    nc = 4;
   }
-  int32_t *chosen = d_chosen;
-  double *met = d_met;
+  int32_t *chosen = io.chosen;
+  double *met = io.met;
   if (!chosen) {
     HIPCHK(c, c->w_sel.ensure(sizeof(int32_t) * B), "hipMalloc(sel)");
     chosen = c->w_sel.as<int32_t>();
@@ -398,16 +426,29 @@ int receive(kml_ctx *c, const double2 *y, const double2 *true_h, double snr, int
   }
   if (c->rc.metric_soft)
     return fail(c, KML_E_UNSUP, "[xcodec] metric_type = true (soft syndrome metric) is not implemented yet");
+  // histogram mode: the counters go to a fresh arena slot (read back like BP's)
+  unsigned long long *hist_cnt = nullptr;
+  if (io.histogram) {
+    bp_slot = next_slot(c);
+    hist_cnt = slot_ptr(c, bp_slot);
+    HIPCHK(c, hipMemsetAsync(hist_cnt, 0, sizeof(unsigned long long) * kml::CNT_N, c->stream), "memset");
+  }
   if (!c->code.is5g) {  // hard metric on the demapper output (kmcodec.cc:109-117)
-    Timer t(c, "metric", -1, (double)B * S * 16.0);
-    HIPCHK(c, kml::launch_cand_metric(c->dc, c->modem.bits, cons, y, S, c->w_h4.as<double2>(), var, B, nullptr, met,
-                                      chosen, c->stream),
+    Timer t(c, "metric", -1, (double)B * nc * S * 16.0);
+    HIPCHK(c, kml::launch_cand_metric(c->dc, c->modem.bits, cons, io.y, S, hc, nc, var, B, met, chosen, c->stream),
            "cand_metric");
     t.stop();
+    if (io.histogram) {
+      if (io.ref_bits)
+        HIPCHK(c, kml::launch_count_packed(io.ref_bits, c->code.Kw, K, nullptr, 0, B, io.cw_err, hist_cnt, c->stream),
+               "count");
+      if (io.uh) HIPCHK(c, hipMemsetAsync(io.uh, 0, (size_t)B * K, c->stream), "memset uh");
+      return KML_OK;
+    }
     HIPCHK(c, c->w_p0.ensure(sizeof(double) * cc * B), "hipMalloc(p0)");
     Timer t2(c, "demap", -1, (double)B * S * (16.0 + 8.0 * c->modem.bits));
-    HIPCHK(c, kml::launch_demap(c->modem.bits, cons, y, S, 1, c->w_h4.as<double2>(), 4, chosen, var, B,
-                                c->w_p0.as<double>(), c->stream),
+    HIPCHK(c, kml::launch_demap(c->modem.bits, cons, io.y, S, 1, hc, nc, chosen, var, B, c->w_p0.as<double>(),
+                                c->stream),
            "demap");
     t2.stop();
     a.p0 = c->w_p0.as<double>();
@@ -415,27 +456,41 @@ int receive(kml_ctx *c, const double2 *y, const double2 *true_h, double snr, int
     return run_bp(c, a, bp_slot);
   }
   // 5G: metric = parity count after metric_iter BP iterations (kmcodec.cc:157-160)
-  HIPCHK(c, c->w_p0.ensure(sizeof(double) * cc * 4 * B), "hipMalloc(p0)");
-  HIPCHK(c, c->w_pc.ensure(sizeof(int32_t) * 4 * B), "hipMalloc(pc)");
+  HIPCHK(c, c->w_p0.ensure(sizeof(double) * cc * nc * B), "hipMalloc(p0)");
+  HIPCHK(c, c->w_pc.ensure(sizeof(int32_t) * nc * B), "hipMalloc(pc)");
   {
-    Timer t(c, "demap", -1, 4.0 * B * S * (16.0 + 8.0 * c->modem.bits));
-    HIPCHK(c, kml::launch_demap(c->modem.bits, cons, y, S, 4, c->w_h4.as<double2>(), 1, nullptr, var, 4 * B,
-                                c->w_p0.as<double>(), c->stream),
-           "demap4");
+    Timer t(c, "demap", -1, (double)nc * B * S * (16.0 + 8.0 * c->modem.bits));
+    HIPCHK(c, kml::launch_demap(c->modem.bits, cons, io.y, S, nc, hc, 1, nullptr, var, nc * B, c->w_p0.as<double>(),
+                                c->stream),
+           "demap candidates");
     t.stop();
   }
   kml::BpLaunch m;
-  m.B = 4 * B;
+  m.B = nc * B;
   m.iter_count = c->rc.metric_iter;
   m.max_iter = c->rc.max_iter;
   m.p0 = c->w_p0.as<double>();
   m.p0_stride = (long long)cc;
   m.parity_cnt = c->w_pc.as<int32_t>();
+  if (io.histogram) {  // keep the candidates' uu_hat: CntErr reads the last one's
+    HIPCHK(c, c->w_uh4.ensure((size_t)nc * B * K), "hipMalloc(uh4)");
+    m.uu_hat = c->w_uh4.as<uint8_t>();
+  }
   int mslot = 0;
   TRY(run_bp(c, m, mslot));
-  HIPCHK(c, kml::launch_select(c->w_pc.as<int32_t>(), B, met, chosen, c->stream), "select");
+  HIPCHK(c, kml::launch_select(c->w_pc.as<int32_t>(), nc, B, met, chosen, c->stream), "select");
+  if (io.histogram) {
+    const uint8_t *last = c->w_uh4.as<uint8_t>() + (size_t)(nc - 1) * K;
+    if (io.ref_bits)
+      HIPCHK(c, kml::launch_count_packed(io.ref_bits, c->code.Kw, K, last, (long long)nc * K, B, io.cw_err, hist_cnt,
+                                         c->stream),
+             "count");
+    if (io.uh)
+      HIPCHK(c, hipMemcpy2DAsync(io.uh, K, last, (size_t)nc * K, K, B, hipMemcpyDeviceToDevice, c->stream), "copy uh");
+    return KML_OK;
+  }
   a.p0 = c->w_p0.as<double>();
-  a.p0_stride = (long long)cc * 4;
+  a.p0_stride = (long long)cc * nc;
   a.p0_sel = chosen;
   a.p0_sel_stride = (long long)cc;
   return run_bp(c, a, bp_slot);
@@ -487,7 +542,7 @@ void kml_destroy(kml_ctx *c) {
     hipStreamSynchronize(c->stream);
     drain_profile(c);
     for (DBuf *b : {&c->d_graph, &c->d_cons, &c->d_arena, &c->d_queue, &c->d_gslots, &c->w_y, &c->w_h, &c->w_h4,
-                    &c->w_hhat, &c->w_p0, &c->w_uu, &c->w_uh, &c->w_ret, &c->w_cch, &c->w_syn, &c->w_sel, &c->w_met,
+                    &c->w_hhat, &c->w_p0, &c->w_uu, &c->w_uh, &c->w_uh4, &c->w_cwerr, &c->w_ret, &c->w_cch, &c->w_syn, &c->w_sel, &c->w_met,
                     &c->w_pc, &c->w_cnt, &c->w_km, &c->s_uu, &c->s_cc, &c->s_y, &c->s_h})
       b->release();
     hipStreamDestroy(c->stream);
@@ -649,8 +704,15 @@ int kml_decode_frames(kml_ctx *c, const double *y, const double *true_h, double 
   TRY(stage_out_ptr(c, c->w_ret, ret, (size_t)B, flags, d_ret));
   TRY(stage_out_ptr(c, c->w_hhat, h_hat, (size_t)B * 2, flags, d_hh));
   int slot;
-  TRY(receive(c, reinterpret_cast<const double2 *>(d_y), reinterpret_cast<const double2 *>(d_h), snr, B, d_uh, d_ch,
-              d_met, d_ret, reinterpret_cast<double2 *>(d_hh), nullptr, slot));
+  RecvIO io;
+  io.y = reinterpret_cast<const double2 *>(d_y);
+  io.true_h = reinterpret_cast<const double2 *>(d_h);
+  io.uh = d_uh;
+  io.chosen = d_ch;
+  io.met = d_met;
+  io.ret = d_ret;
+  io.hhat = reinterpret_cast<double2 *>(d_hh);
+  TRY(receive(c, io, snr, B, slot));
   if (true_h) {  // single candidate: chosen = 0, metrics unset (kmcodec.cc:66-67)
     if (chosen && !(flags & KML_DEVICE_PTRS)) memset(chosen, 0, sizeof(int32_t) * B);
     if (metrics && !(flags & KML_DEVICE_PTRS)) memset(metrics, 0, sizeof(double) * 4 * B);
@@ -714,6 +776,23 @@ int kml_sim_generate(kml_ctx *c, double snr, uint64_t seed, uint64_t first_cw, i
   return sync(c);
 }
 
+namespace {
+int sim_receive(kml_ctx *c, double snr, int blind, bool histogram, int &slot) {
+  RecvIO io;
+  io.y = c->s_y.as<double2>();
+  io.true_h = blind ? nullptr : c->s_h.as<double2>();
+  io.ref_bits = c->s_uu.as<uint64_t>();
+  HIPCHK(c, c->w_cwerr.ensure(sizeof(int32_t) * (size_t)c->sim_B), "hipMalloc(cw_err)");
+  io.cw_err = c->w_cwerr.as<int32_t>();
+  io.histogram = histogram;
+  if (histogram) {
+    HIPCHK(c, c->w_met.ensure(sizeof(double) * 4 * (size_t)c->sim_B), "hipMalloc(met)");
+    io.met = c->w_met.as<double>();
+  }
+  return receive(c, io, snr, c->sim_B, slot);
+}
+}  // namespace
+
 int kml_sim_decode(kml_ctx *c, double snr, int blind, uint64_t *counters, int do_sync) {
   if (!c) return KML_E_ARG;
   if (!do_sync && counters) return fail(c, KML_E_ARG, "counters need sync != 0");
@@ -722,13 +801,63 @@ int kml_sim_decode(kml_ctx *c, double snr, int blind, uint64_t *counters, int do
   const int B = c->sim_B;
   if (B == 0) return KML_OK;
   int slot = 0;
-  TRY(receive(c, c->s_y.as<double2>(), blind ? nullptr : c->s_h.as<double2>(), snr, B, nullptr, nullptr, nullptr,
-              nullptr, nullptr, c->s_uu.as<uint64_t>(), slot));
+  TRY(sim_receive(c, snr, blind, false, slot));
   if (counters) {
     unsigned long long h[kml::CNT_N];
     HIPCHK(c, hipMemcpyAsync(h, slot_ptr(c, slot), sizeof(h), hipMemcpyDeviceToHost, c->stream), "D2H");
     TRY(sync(c));
     for (int i = 0; i < kml::CNT_N; i++) counters[i] = h[i];
+  }
+  return KML_OK;
+}
+
+int kml_sim_decode_ex(kml_ctx *c, double snr, int blind, int histogram, int32_t *cw_err, double *metrics,
+                      uint64_t *counters) {
+  if (!c) return KML_E_ARG;
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const int B = c->sim_B;
+  if (B == 0) {
+    if (counters) memset(counters, 0, sizeof(uint64_t) * kml::CNT_N);
+    return KML_OK;
+  }
+  int slot = 0;
+  TRY(sim_receive(c, snr, blind, histogram != 0, slot));
+  unsigned long long h[kml::CNT_N];
+  HIPCHK(c, hipMemcpyAsync(h, slot_ptr(c, slot), sizeof(h), hipMemcpyDeviceToHost, c->stream), "D2H");
+  if (cw_err)
+    HIPCHK(c, hipMemcpyAsync(cw_err, c->w_cwerr.p, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream), "D2H");
+  if (metrics) {
+    if (histogram)
+      HIPCHK(c, hipMemcpyAsync(metrics, c->w_met.p, sizeof(double) * 4 * B, hipMemcpyDeviceToHost, c->stream), "D2H");
+    else
+      memset(metrics, 0, sizeof(double) * 4 * B);
+  }
+  TRY(sync(c));
+  if (counters)
+    for (int i = 0; i < kml::CNT_N; i++) counters[i] = h[i];
+  return KML_OK;
+}
+
+int kml_run_config(const kml_ctx *c, double *f, int64_t *n) {
+  if (!c) return KML_E_ARG;
+  const kml::RunConfig &r = c->rc;
+  if (f) {
+    f[0] = r.min_snr;
+    f[1] = r.max_snr;
+    f[2] = r.step_snr;
+  }
+  if (n) {
+    n[0] = r.max_err_blk;
+    n[1] = r.max_num_blk;
+    n[2] = r.thread_num_blk;
+    n[3] = r.known_h ? 1 : 0;
+    n[4] = r.is5g ? 1 : 0;
+    n[5] = r.metric_soft ? 1 : 0;
+    n[6] = r.metric_iter;
+    n[7] = r.histogram ? 1 : 0;
+    n[8] = r.max_iter;
+    n[9] = r.active ? 1 : 0;
   }
   return KML_OK;
 }

@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void demap_kernel(const double *__restrict__ c
 template <int MB>
 __global__ __launch_bounds__(256) void cand_metric_kernel(DevCode c, const double *__restrict__ cons,
                                                           const double2 *__restrict__ y, int S,
-                                                          const double2 *__restrict__ h4, double var,
+                                                          const double2 *__restrict__ h4, int nc, double var,
                                                           double *__restrict__ metrics, int32_t *__restrict__ chosen) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int *cnt = reinterpret_cast<int *>(smem);  // 4 counters
@@ -121,7 +121,8 @@ __global__ __launch_bounds__(256) void cand_metric_kernel(DevCode c, const doubl
     const double2 v = yy[j];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const double2 hh = h4[(long long)cw * 4 + q];
+      if (q >= nc) break;
+      const double2 hh = h4[(long long)cw * nc + q];
       double out[MB];
       demap_symbol<MB>(cons, v.x, v.y, hh.x, hh.y, var, out);
 #pragma unroll
@@ -135,7 +136,8 @@ __global__ __launch_bounds__(256) void cand_metric_kernel(DevCode c, const doubl
     for (int e = c.row_ptr[r]; e < c.row_ptr[r + 1]; ++e) {
       const int col = c.row_col[e];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) p[q] ^= hb[q * c.cc_len + col];
+      for (int q = 0; q < 4; ++q)
+        if (q < nc) p[q] ^= hb[q * c.cc_len + col];
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) local[q] += p[q];
@@ -147,23 +149,50 @@ __global__ __launch_bounds__(256) void cand_metric_kernel(DevCode c, const doubl
   if (tid == 0) {
     int best = 0;
     for (int q = 0; q < 4; ++q) {
-      metrics[(long long)cw * 4 + q] = fabs((double)cnt[q]);
-      if (cnt[q] < cnt[best]) best = q;
+      metrics[(long long)cw * 4 + q] = q < nc ? fabs((double)cnt[q]) : 0.0;
+      if (q < nc && cnt[q] < cnt[best]) best = q;
     }
     chosen[cw] = best;
   }
 }
 
-__global__ void select_kernel(const int32_t *__restrict__ pc, int B, double *__restrict__ metrics,
+__global__ void select_kernel(const int32_t *__restrict__ pc, int nc, int B, double *__restrict__ metrics,
                               int32_t *__restrict__ chosen) {
   const int cw = blockIdx.x * blockDim.x + threadIdx.x;
   if (cw >= B) return;
   int best = 0;
   for (int q = 0; q < 4; ++q) {
-    metrics[(long long)cw * 4 + q] = fabs((double)pc[(long long)cw * 4 + q]);
-    if (pc[(long long)cw * 4 + q] < pc[(long long)cw * 4 + best]) best = q;
+    metrics[(long long)cw * 4 + q] = q < nc ? fabs((double)pc[(long long)cw * nc + q]) : 0.0;
+    if (q < nc && pc[(long long)cw * nc + q] < pc[(long long)cw * nc + best]) best = q;
   }
   chosen[cw] = best;
+}
+
+// SourceSink::CntErr (sourcesink.cc:29-47) of byte decisions uh (NULL = all
+// zero) against bit-packed reference words; one wave per codeword.
+__global__ __launch_bounds__(64) void count_packed_kernel(const uint64_t *__restrict__ ref, int Kw, int K,
+                                                          const uint8_t *__restrict__ uh, long long uh_stride, int B,
+                                                          int32_t *__restrict__ cw_err,
+                                                          unsigned long long *__restrict__ counters) {
+  const int cw = blockIdx.x;
+  const int lane = threadIdx.x;
+  int errs = 0;
+  for (int w = lane; w < Kw; w += 64) {
+    uint64_t word = 0;
+    const int base = w * 64;
+    const int nb = min(64, K - base);
+    if (uh)
+      for (int j = 0; j < nb; ++j) word |= (uint64_t)(uh[(long long)cw * uh_stride + base + j] & 1) << j;
+    errs += __popcll(word ^ ref[(long long)cw * Kw + w]);
+  }
+  for (int off = 32; off > 0; off >>= 1) errs += __shfl_xor(errs, off);
+  if (lane == 0) {
+    if (cw_err) cw_err[cw] = errs;
+    atomicAdd(&counters[CNT_ERR_BIT], (unsigned long long)errs);
+    atomicAdd(&counters[CNT_ERR_BLK], errs > 0 ? 1ull : 0ull);
+    atomicAdd(&counters[CNT_TOT_BIT], (unsigned long long)K);
+    atomicAdd(&counters[CNT_TOT_BLK], 1ull);
+  }
 }
 
 __global__ void count_bytes_kernel(const uint8_t *__restrict__ uu, const uint8_t *__restrict__ uh, int K, int B,
@@ -204,9 +233,10 @@ hipError_t launch_demap(int bits, const double *cons, const double2 *y, int S, i
 }
 
 hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, const double2 *y, int S,
-                              const double2 *h4, double var, int B, uint64_t * /*hard_ws*/, double *metrics,
-                              int32_t *chosen, hipStream_t s) {
+                              const double2 *h4, int nc, double var, int B, double *metrics, int32_t *chosen,
+                              hipStream_t s) {
   if (B == 0) return hipSuccess;
+  if (nc < 1 || nc > 4) return hipErrorInvalidValue;
   const size_t lds = 16 + 4 * (size_t)c.cc_len;
   const dim3 grid(B), blk(256);
   switch (bits) {
@@ -215,7 +245,7 @@ hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, co
     hipError_t e = hipFuncSetAttribute((const void *)cand_metric_kernel<MBV>,                                \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
     if (e != hipSuccess) return e;                                                                           \
-    hipLaunchKernelGGL(cand_metric_kernel<MBV>, grid, blk, lds, s, c, cons, y, S, h4, var, metrics, chosen); \
+    hipLaunchKernelGGL(cand_metric_kernel<MBV>, grid, blk, lds, s, c, cons, y, S, h4, nc, var, metrics, chosen); \
     break;                                                                                                   \
   }
     KML_CM(1)
@@ -230,9 +260,16 @@ hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, co
   return hipGetLastError();
 }
 
-hipError_t launch_select(const int32_t *parity_cnt, int B, double *metrics, int32_t *chosen, hipStream_t s) {
+hipError_t launch_select(const int32_t *parity_cnt, int nc, int B, double *metrics, int32_t *chosen, hipStream_t s) {
   if (B == 0) return hipSuccess;
-  hipLaunchKernelGGL(select_kernel, dim3((B + 255) / 256), dim3(256), 0, s, parity_cnt, B, metrics, chosen);
+  hipLaunchKernelGGL(select_kernel, dim3((B + 255) / 256), dim3(256), 0, s, parity_cnt, nc, B, metrics, chosen);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_packed(const uint64_t *ref, int Kw, int K, const uint8_t *uh, long long uh_stride, int B,
+                               int32_t *cw_err, unsigned long long *counters, hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  hipLaunchKernelGGL(count_packed_kernel, dim3(B), dim3(64), 0, s, ref, Kw, K, uh, uh_stride, B, cw_err, counters);
   return hipGetLastError();
 }
 

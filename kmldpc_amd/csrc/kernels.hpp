@@ -54,6 +54,7 @@ struct BpLaunch {
   int32_t *parity_cnt = nullptr; // [B] unsatisfied checks of the final cc_hat
   const uint64_t *ref_bits = nullptr;  // [B][Kw] for error counting
   unsigned long long *counters = nullptr;  // [CNT_N]
+  int32_t *cw_err = nullptr;     // [B] error bits per codeword vs ref_bits (stop-rule prefix)
   double2 *gslots = nullptr;     // global slot scratch when E*16 exceeds LDS
   long long gslots_cap = 0;      // number of double2 available
   unsigned int *queue = nullptr; // 4-byte device dequeue counter (zeroed by the launcher)
@@ -79,13 +80,19 @@ hipError_t launch_demap(int bits, const double *cons, const double2 *y, int S, i
                         int h_stride, const int32_t *h_sel, double var, int n, double *p0, hipStream_t s);
 
 // Hard-metric candidates for the PEG blind path (kmcodec.cc:105-119):
-// for each codeword and each of the 4 rotated estimates h4[b][j], the number of
-// unsatisfied checks of rr = (P0 > 0.5).  metrics[b][4] doubles, chosen[b].
+// for each codeword and each of its nc (1 or 4) channel estimates h4[b][j], the
+// number of unsatisfied checks of rr = (P0 > 0.5).  metrics[b][4] doubles
+// (entries >= nc zeroed), chosen[b] = first argmin.
 hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, const double2 *y, int S,
-                              const double2 *h4, double var, int B, uint64_t *hard_ws, double *metrics,
-                              int32_t *chosen, hipStream_t s);
-// argmin over a [B][4] metric table (first minimum) for the BP-based metrics.
-hipError_t launch_select(const int32_t *parity_cnt, int B, double *metrics, int32_t *chosen, hipStream_t s);
+                              const double2 *h4, int nc, double var, int B, double *metrics, int32_t *chosen,
+                              hipStream_t s);
+// argmin over a [B][nc] parity-count table (first minimum) for the BP-based
+// metrics; metrics[b][4] = |count|.
+hipError_t launch_select(const int32_t *parity_cnt, int nc, int B, double *metrics, int32_t *chosen, hipStream_t s);
+// CntErr of byte decisions (uh == NULL: all-zero decisions) against packed
+// reference bits; optional per-codeword error bits.
+hipError_t launch_count_packed(const uint64_t *ref, int Kw, int K, const uint8_t *uh, long long uh_stride, int B,
+                               int32_t *cw_err, unsigned long long *counters, hipStream_t s);
 
 // KMeans::Run + h_hat = clusters[0]/c[0] + 4 rotations (kmeans.hip).
 struct KmState {
