@@ -23,6 +23,11 @@
 //                FMA-capable host — the one the reference's demapper calls
 //                (lib/lab/src/modemlinearsystem.cc:61).  The 2^(k/128) table is
 //                regenerated from first principles (tools/gen_exp_table.py).
+//   kml_log    — glibc >= 2.28 log (sysdeps/ieee754/dbl-64/e_log.c, ARM
+//                optimized-routines: N = 128 table, degree-6 polynomial, a
+//                degree-12 one near 1), again in the contraction pattern of the
+//                FMA ifunc variant (__log_fma).  Used by the soft syndrome
+//                metric (src/kmcodec.cc:155).  Table from tools/gen_log_table.py.
 //   kml_cmul   — std::complex<double> operator* as GCC expands it without
 //                -ffast-math: (ac - bd, ad + bc); the __muldc3 fallback is
 //                reached only when both parts are NaN.
@@ -43,6 +48,7 @@
 #include <cstdint>
 
 #include "exp_table.hpp"
+#include "log_table.hpp"
 
 namespace kml {
 
@@ -218,6 +224,79 @@ KML_HD double kml_exp_t(double x) {
 }
 
 KML_HD double kml_exp(double x) { return kml_exp_t<true>(x); }
+
+KML_HD double log_tab(int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return as_f64(kLogTabDev[i]);
+#else
+  return as_f64(kLogTabHost[i]);
+#endif
+}
+
+template <bool FMA>
+KML_HD double kml_log_t(double x) {
+  const double A[5] = {KML_LOG_POLY_INIT};
+  const double B[11] = {KML_LOG_POLY1_INIT};
+  const double Ln2hi = 0x1.62e42fefa3800p-1, Ln2lo = 0x1.ef35793c76730p-45;
+  const uint64_t OFF = 0x3fe6000000000000ull;
+  uint64_t ix = as_u64(x);
+  const uint32_t top = (uint32_t)(ix >> 48);
+  const uint64_t LO = as_u64(1.0 - 0x1p-4), HI = as_u64(1.0 + 0x1.09p-4);
+  if (ix - LO < HI - LO) {  // close to 1
+    if (ix == as_u64(1.0)) return 0.0;
+    const double r = x - 1.0;
+    const double r2 = r * r;
+    const double r3 = r * r2;
+    double p;  // y = r3 * p
+    if (FMA) {
+      const double p3 = fma(r3, B[10], fma(r2, B[9], fma(r, B[8], B[7])));
+      const double p2 = fma(r3, p3, fma(r2, B[6], fma(r, B[5], B[4])));
+      p = fma(r3, p2, fma(r2, B[3], fma(r, B[2], B[1])));
+    } else {
+      p = B[1] + r * B[2] + r2 * B[3] + r3 * (B[4] + r * B[5] + r2 * B[6] + r3 * (B[7] + r * B[8] + r2 * B[9] + r3 * B[10]));
+    }
+    double w = r * 0x1p27;
+    const double rhi = r + w - w;
+    const double rlo = r - rhi;
+    w = rhi * rhi * B[0];
+    const double hi = r + w;
+    double lo = r - hi + w;
+    lo = FMA ? fma(B[0] * rlo, rhi + r, lo) : lo + B[0] * rlo * (rhi + r);
+    // y = r3*p; y += lo; y += hi — the FMA build fuses the first add
+    const double y = FMA ? fma(r3, p, lo) : r3 * p + lo;
+    return y + hi;
+  }
+  if (top - 0x0010 >= 0x7ff0 - 0x0010) {
+    if (ix * 2 == 0) return -1.0 / 0.0;        // log(+-0) = -inf, divide-by-zero
+    if (ix == as_u64(INFINITY)) return x;    // log(inf) = inf
+    if ((top & 0x8000) || (top & 0x7ff0) == 0x7ff0) return (x - x) / (x - x);  // negative or NaN
+    ix = as_u64(x * 0x1p52);                 // subnormal: normalise
+    ix -= 52ull << 52;
+  }
+  const uint64_t tmp = ix - OFF;
+  const int i = (int)((tmp >> (52 - 7)) % 128);
+  const int k = (int)((int64_t)tmp >> 52);
+  const uint64_t iz = ix - (tmp & (0xfffull << 52));
+  const double invc = log_tab(4 * i), logc = log_tab(4 * i + 1);
+  const double z = as_f64(iz);
+  double r;
+  if (FMA)
+    r = fma(z, invc, -1.0);
+  else
+    r = (z - log_tab(4 * i + 2) - log_tab(4 * i + 3)) * invc;
+  const double kd = (double)k;
+  const double w = FMA ? fma(kd, Ln2hi, logc) : kd * Ln2hi + logc;
+  const double hi = w + r;
+  const double lo = FMA ? fma(kd, Ln2lo, w - hi + r) : w - hi + r + kd * Ln2lo;
+  const double r2 = r * r;
+  if (FMA) {
+    const double p = fma(r2, fma(r, A[4], A[3]), fma(r, A[2], A[1]));
+    return fma(r * r2, p, fma(r2, A[0], lo)) + hi;
+  }
+  return lo + r2 * A[0] + r * r2 * (A[1] + r * A[2] + r2 * (A[3] + r * A[4])) + hi;
+}
+
+KML_HD double kml_log(double x) { return kml_log_t<true>(x); }
 
 KML_HD cplx kml_cmul(cplx a, cplx b) { return cplx{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
 

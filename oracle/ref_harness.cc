@@ -12,6 +12,8 @@
 // The output is a flat little-endian record stream consumed by
 // tests/golden/make_golden.py.  Nothing here is copied from the reference; the
 // harness only calls its public methods.
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -44,7 +46,7 @@ static void put_bits(FILE *f, const int *v, int n) {
 int main(int argc, char **argv) {
   if (argc < 5) {
     fprintf(stderr, "usage: %s config.toml snr n_codewords out.bin [mode]\n", argv[0]);
-    fprintf(stderr, "  mode: frames (default) | simulate\n");
+    fprintf(stderr, "  mode: frames (default) | simulate | soft | softhist\n");
     return 2;
   }
   const std::string cfg = argv[1];
@@ -151,6 +153,85 @@ int main(int argc, char **argv) {
     put_f64(f, ber);
     put_f64(f, ssink.fer());
     fclose(f);
+    return 0;
+  }
+
+  if (mode == "soft" || mode == "softhist") {
+    // Soft syndrome metric ([xcodec] metric_type = true).  The metric depends
+    // on the codec's syndrom_soft_ history (rows are only rewritten when a CN
+    // phase runs), so the call sequence must be exactly the simulator's:
+    //   soft     : KmCodec::Decoder only (simulator.cc:164); the candidate
+    //              metrics and the chosen index are recovered from the codec's
+    //              own log records ("Hhat = ... Metric = %.14f", "hatIndex = ").
+    //   softhist : KmCodec::GetHistogramData only (histogram mode,
+    //              simulator.cc:155); metrics are returned exactly, and uu_hat
+    //              is what the last metric decode left.
+    std::ostringstream cap;
+    std::ofstream null3("/dev/null");
+    lab::logger::TeeStream tee2(cap, null3);
+    lab::logger::Log::get().set_log_stream(tee2);
+    std::vector<int> uu(K), cc(N), uu_hat(K, 0);
+    for (int i = 0; i < ncw; i++) {
+      lab::SourceSink ssink;
+      ssink.GetBitStr(uu.data(), K);
+      codec.Encoder(uu.data(), cc.data());
+      std::complex<double> true_h;
+      lab::CLCRandNum::Get().Normal(true_h);
+      true_h *= sqrt(0.5);
+      std::vector<std::complex<double>> gh(1, true_h);
+      mls.PartitionModemLSystem(cc.data(), gh);
+      auto y = mls.GetRecvSymbol();
+      std::vector<std::complex<double>> h_hats;
+      std::complex<double> h_hat(0, 0);
+      if (known_h) {
+        h_hats.push_back(true_h);
+      } else {
+        auto constellations = mls.constellations();
+        kmldpc::KMeans km(y, constellations, 20);
+        km.Run();
+        auto cl = km.clusters();
+        h_hat = cl[0] / constellations[0];
+        for (size_t j = 0; j < 4; j++)
+          h_hats.push_back(h_hat * exp(std::complex<double>(0, (lab::kPi / 2) * j)));
+      }
+      std::vector<double> metrics(4, 0.0);
+      int chosen = 0;
+      cap.str("");
+      cap.clear();
+      if (mode == "softhist") {
+        auto m = codec.GetHistogramData(mls, h_hats, uu_hat.data());
+        for (size_t j = 0; j < m.size(); j++) metrics[j] = m[j];
+        chosen = (int)std::distance(m.begin(), std::min_element(m.begin(), m.end()));
+      } else {
+        codec.Decoder(mls, h_hats, uu_hat.data());
+        std::string line;
+        std::istringstream in(cap.str());
+        int j = 0;
+        while (std::getline(in, line)) {
+          size_t k = line.find("Metric = ");
+          if (k != std::string::npos && j < 4) metrics[j++] = fabs(strtod(line.c_str() + k + 9, nullptr));
+          k = line.find("hatIndex = ");
+          if (k != std::string::npos) chosen = atoi(line.c_str() + k + 11);
+        }
+      }
+      int errs = 0;
+      for (int t = 0; t < K; t++) errs += (uu[t] != uu_hat[t]);
+      put_bits(f, uu.data(), K);
+      put_f64(f, true_h.real());
+      put_f64(f, true_h.imag());
+      for (auto &v : y) {
+        put_f64(f, v.real());
+        put_f64(f, v.imag());
+      }
+      put_f64(f, h_hat.real());
+      put_f64(f, h_hat.imag());
+      for (int j = 0; j < 4; j++) put_f64(f, metrics[j]);
+      put_i32(f, chosen);
+      put_bits(f, uu_hat.data(), K);
+      put_i32(f, errs);
+    }
+    fclose(f);
+    delete direct;
     return 0;
   }
 

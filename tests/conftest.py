@@ -76,3 +76,13 @@ def write_config(path, data_dir, matrix, modem, is5g=False, known=True, max_iter
     modem_file = "{os.path.join(data_dir, modem)}"
 """)
     return path
+
+
+def soft_case_names():
+    d = os.path.join(GOLDEN, "soft")
+    return sorted(f[:-4] for f in os.listdir(d) if f.endswith(".npz")) if os.path.isdir(d) else []
+
+
+def load_soft_case(name):
+    z = np.load(os.path.join(GOLDEN, "soft", name + ".npz"))
+    return json.loads(bytes(z["hdr_json"]).decode()), z

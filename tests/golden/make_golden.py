@@ -56,13 +56,23 @@ CASES = {
     "peg2304_16qamphi1_blind": ("PEG2304regular0.5.txt", "4bit_16QAM_phi1.txt", False, False, 20, 8.0, 100, True),
 }
 
+# soft syndrome metric ([xcodec] metric_type = true): name -> (matrix, modem, 5g,
+# known_h, max_iter, snr, n_cw, metric_iter, harness mode); written to soft/<name>.npz
+SOFT_CASES = {
+    "peg2304_qpsk_soft": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.0, 300, 5, "soft"),
+    "peg2304_qpsk_soft_hisnr": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 4.0, 300, 5, "soft"),
+    "peg2304_qpsk_softhist": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 3.0, 300, 5, "softhist"),
+    "bg2_16qam_soft": ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, False, 50, 5.01, 100, 5, "soft"),
+    "peg2304_16qam_soft_it3": ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", False, False, 20, 7.0, 150, 3, "soft"),
+}
+
 COUNTER_CASES = {
     "peg2304_qpsk_known_2000": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, True, 20, 2.0, 2000, True),
     "peg2304_qpsk_blind_2000": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.0, 2000, True),
 }
 
 
-def write_toml(path, data_dir, matrix, modem, is5g, known, max_iter, active, metric_iter=5):
+def write_toml(path, data_dir, matrix, modem, is5g, known, max_iter, active, metric_iter=5, soft=False):
     b = lambda v: "true" if v else "false"
     with open(path, "w") as f:
         f.write(f"""[range]
@@ -76,7 +86,7 @@ def write_toml(path, data_dir, matrix, modem, is5g, known, max_iter, active, met
     true_h_arg = {b(known)}
 [xcodec]
     5gldpc = {b(is5g)}
-    metric_type = false
+    metric_type = {b(soft)}
     metric_iter = {metric_iter}
 [histogram]
     enable = false
@@ -149,7 +159,58 @@ def parse_frames(buf):
     return hdr, cons, recs
 
 
+def parse_soft(buf):
+    """Records of ref_harness modes soft / softhist."""
+    r = Reader(buf)
+    magic, K, N, S, M, Kc, known, is5g, max_iter, ncw = [r.i32() for _ in range(10)]
+    snr = r.f64()
+    r.f64(2 * Kc)
+    recs = []
+    for _ in range(ncw):
+        d = {"uu": r.u8(K)}
+        d["true_h"] = r.f64(2)
+        d["y"] = r.f64(2 * S).reshape(S, 2)
+        d["h_hat"] = r.f64(2)
+        d["metrics"] = r.f64(4)
+        d["chosen"] = r.i32()
+        d["uu_hat"] = r.u8(K)
+        d["errs"] = r.i32()
+        recs.append(d)
+    return dict(K=K, N=N, S=S, M=M, known=known, is5g=is5g, max_iter=max_iter, snr=snr), recs
+
+
+def make_soft(tmp):
+    os.makedirs(os.path.join(HERE, "soft"), exist_ok=True)
+    for name, (mat, mod, is5g, known, it, snr, n, mit, mode) in SOFT_CASES.items():
+        cfg = os.path.join(tmp, name + ".toml")
+        write_toml(cfg, REF_CFG, mat, mod, is5g, known, it, True, metric_iter=mit, soft=True)
+        out = os.path.join(tmp, name + ".bin")
+        subprocess.run([HARNESS, cfg, repr(snr), str(n), out, mode], check=True)
+        hdr, recs = parse_soft(open(out, "rb").read())
+        hdr.update(matrix=mat, modem=mod, metric_iter=mit, mode=mode)
+        # frames are regenerated by the oracle (same seed-17 stream as the
+        # frames cases); only their CRCs are kept
+        arrs = {"hdr_json": np.frombuffer(json.dumps(hdr).encode(), dtype=np.uint8)}
+        arrs["crc_y"] = np.array([crc(d["y"]) for d in recs], np.uint32)
+        arrs["crc_uu"] = np.array([crc(d["uu"]) for d in recs], np.uint32)
+        for key in ["true_h", "h_hat", "metrics"]:
+            arrs[key] = np.stack([d[key] for d in recs])
+        arrs["uu_hat_bits"] = np.packbits(np.stack([d["uu_hat"] for d in recs]), axis=1)
+        arrs["chosen"] = np.array([d["chosen"] for d in recs], np.int32)
+        arrs["errs"] = np.array([d["errs"] for d in recs], np.int32)
+        np.savez_compressed(os.path.join(HERE, "soft", name + ".npz"), **arrs)
+        print(f"{name}: n={n} FER={np.mean(arrs['errs'] > 0):.4f} chosen={np.bincount(arrs['chosen'], minlength=4)} "
+              f"inf_metrics={int(np.isinf(arrs['metrics']).sum())}")
+
+
 def main():
+    if "--soft" in sys.argv:
+        tmp = tempfile.mkdtemp()
+        try:
+            make_soft(tmp)
+        finally:
+            shutil.rmtree(tmp)
+        return
     if not os.path.exists(HARNESS):
         sys.exit("build oracle/_ref/ref_harness first (make -C oracle ref)")
     ddir = os.path.join(HERE, "data")

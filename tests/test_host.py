@@ -172,3 +172,15 @@ def test_exp_host_restatement(tmp_path):
     out = subprocess.run([str(exe), "2000000"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
     assert "exp_fma_mismatch=0" in out.stdout
+
+
+def test_log_host_restatement(tmp_path):
+    """kml_log (glibc's table-driven log, FMA-variant contraction pattern,
+    constants from tools/gen_log_table.py) equals the host glibc log, including
+    the close-to-1 branch, subnormals and special values."""
+    exe = tmp_path / "logc"
+    src = os.path.join(REPO, "tests", "native", "log_check.cpp")
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", "-o", str(exe), src], check=True)
+    out = subprocess.run([str(exe), "2000000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    assert "log_fma_mismatch=0" in out.stdout

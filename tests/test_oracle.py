@@ -5,6 +5,7 @@ The golden fixtures were produced by running the reference sources
 seed 17; see tests/golden/make_golden.py.  These tests need no GPU.
 """
 import json
+import math
 import os
 import zlib
 
@@ -128,3 +129,66 @@ def test_copy_constructed_row_order_same_decisions(data_dir):
         ra, ua, _, _ = a.bp_decode(z["v_p0"][i])
         rb, ub, _, _ = b.bp_decode(z["v_p0"][i])
         assert ra == rb and np.array_equal(ua, ub)
+
+
+# ---------------------------------------------------------------- soft metric
+from conftest import load_soft_case, soft_case_names  # noqa: E402
+
+
+def oracle_soft_stream(code, modem, hdr, y, n):
+    """The oracle run the way the reference's codec instance sees it: one
+    syndrom_soft buffer carried across every decode of the stream (initially
+    zeros), KmCodec::Decoder (mode soft) or GetHistogramData only (softhist)."""
+    syn = np.zeros(code.M)
+    var = 10 ** (-0.1 * hdr["snr"])
+    out = []
+    for i in range(n):
+        if hdr["mode"] == "soft":
+            r = O.receive(code, modem, y[i], np.zeros(2), hdr["snr"], True, metric_soft=True,
+                          metric_iter=hdr["metric_iter"], syn=syn)
+            out.append((r["metrics"], r["chosen"], r["uu_hat"]))
+        else:
+            hh = O.kmeans_hhat(y[i], modem.points)
+            h4 = O.rotations(hh)
+            met = np.zeros(4)
+            uh = None
+            for j in range(4):
+                p0 = modem.demap(y[i], h4[j], var)
+                _, uh, _, syn = code.bp_decode(p0, hdr["metric_iter"], syn=syn)
+                mt = 0.0
+                for v in syn:
+                    mt += math.log(v)  # glibc log, like the reference
+                met[j] = abs(mt)
+            out.append((met, int(np.argmin(met)), uh))
+    return out
+
+
+def soft_frames(code, modem, hdr, z, n):
+    """The fixture stream's frames, regenerated by the oracle (seed 17) and
+    checked against the reference's CRCs."""
+    uu, cc, th, y = O.gen_frames(code, modem, hdr["snr"], n)
+    for i in range(n):
+        assert crc(y[i]) == z["crc_y"][i] and crc(uu[i].astype(np.uint8)) == z["crc_uu"][i], i
+    return uu, y
+
+
+def soft_uu_hat(z, n, K):
+    return np.unpackbits(z["uu_hat_bits"][:n], axis=1)[:, :K]
+
+
+@pytest.mark.parametrize("case", soft_case_names())
+def test_soft_metric_stream_matches_reference(case, data_dir):
+    hdr, z = load_soft_case(case)
+    code = O.Code(os.path.join(data_dir, hdr["matrix"]), bool(hdr["is5g"]), True, False, hdr["max_iter"])
+    modem = O.Modem(os.path.join(data_dir, hdr["modem"]))
+    n = min(len(z["chosen"]), 60)
+    uu, y = soft_frames(code, modem, hdr, z, n)
+    want_uh = soft_uu_hat(z, n, hdr["K"])
+    res = oracle_soft_stream(code, modem, hdr, y, n)
+    for i, (met, ch, uh) in enumerate(res):
+        assert ch == z["chosen"][i], (case, i)
+        assert np.array_equal(uh, want_uh[i]), (case, i)
+        if hdr["mode"] == "softhist":  # returned exactly by GetHistogramData
+            assert np.array_equal(met, z["metrics"][i]), (case, i)
+        else:  # parsed from the codec's "%.14f" log records
+            assert np.allclose(met, z["metrics"][i], rtol=0, atol=6e-15 * np.maximum(1, np.abs(met))), (case, i)
