@@ -55,7 +55,13 @@ enum {
   KML_E_NOMEM = -5
 };
 
-enum { KML_DEVICE_PTRS = 1 };
+enum {
+  KML_DEVICE_PTRS = 1,
+  /* kml_decode_frames: KmCodec::GetHistogramData instead of Decoder — the
+   * candidate metrics only, no final decode; uu_hat is what the last metric
+   * decode left (BP-based metrics) or zeros (hard PEG metric). */
+  KML_HISTOGRAM = 2
+};
 
 typedef struct kml_ctx kml_ctx;
 
@@ -205,6 +211,8 @@ int kml_prof_read_flops(kml_ctx *ctx, const char *stage, double *alg_flops);
  * out[n][4] = (hypot(a,b), re((a+ib)/(c+id)), im(...), exp(a)) with the
  * glibc-exact restatements the kernels use. */
 int kml_math_probe(kml_ctx *ctx, const double *in, int n, double *out);
+/* Device-side probe of the soft metric's log (kml_log, glibc-exact): out[i] = log(in[i]). */
+int kml_log_probe(kml_ctx *ctx, const double *in, int n, double *out);
 /* Device-side probe of the decoder's shared-reciprocal division: in[n][3] =
  * (n0, n1, s) -> out[n][4] = (fast n0/s, fast n1/s, IEEE n0/s, IEEE n1/s). */
 int kml_div_probe(kml_ctx *ctx, const double *in, int n, double *out);

@@ -29,6 +29,7 @@ LIB_PATH = os.path.join(HERE, "libkmldpc_amd.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include", "kmldpc_amd.h")
 
 KML_DEVICE_PTRS = 1
+KML_HISTOGRAM = 2
 DIM_NAMES = ["M", "Ncol", "K", "cc_len", "Z", "E", "chk", "max_iter", "bits", "Kc", "S", "bp_lds"]
 
 
@@ -89,6 +90,7 @@ def lib():
         "kml_prof_read_flops": (I, [P, C.c_char_p, P]),
         "kml_math_probe": (I, [P, P, I, P]),
         "kml_div_probe": (I, [P, P, I, P]),
+        "kml_log_probe": (I, [P, P, I, P]),
         "kml_sim_decode_ex": (I, [P, D, I, I, P, P, P]),
         "kml_run_config": (I, [P, P, P]),
         "kml_sweep_point": (I, [C.POINTER(PointCfg), BATCH_FN, P, ALLREDUCE_FN, P, REPORT_FN, P, P]),
@@ -231,8 +233,9 @@ class Context:
         self._chk(lib().kml_kmeans(self._h, _p(y), B, int(iters), _p(hh), _p(h4), 0), "kml_kmeans")
         return hh, h4
 
-    def decode_frames(self, y, snr, true_h=None):
-        """KmCodec::Decoder: known channel if true_h is given, else the blind path."""
+    def decode_frames(self, y, snr, true_h=None, histogram=False):
+        """KmCodec::Decoder: known channel if true_h is given, else the blind path.
+        histogram=True runs KmCodec::GetHistogramData instead (metrics, no final decode)."""
         y = _f64(y).reshape(-1, self.S, 2)
         B = y.shape[0]
         th = None if true_h is None else _f64(true_h).reshape(B, 2)
@@ -242,7 +245,7 @@ class Context:
         ret = np.zeros(B, np.int32)
         hh = np.zeros((B, 2))
         self._chk(lib().kml_decode_frames(self._h, _p(y), _p(th), float(snr), B, _p(uh), _p(ch), _p(met), _p(ret),
-                                          _p(hh), 0), "kml_decode_frames")
+                                          _p(hh), KML_HISTOGRAM if histogram else 0), "kml_decode_frames")
         return dict(uu_hat=uh, chosen=ch, metrics=met, ret=ret, h_hat=hh)
 
     def count_errors(self, uu, uu_hat):
@@ -324,6 +327,12 @@ class Context:
         x = _f64(x).reshape(-1, 3)
         out = np.zeros((x.shape[0], 4))
         self._chk(lib().kml_div_probe(self._h, _p(x), x.shape[0], _p(out)), "kml_div_probe")
+        return out
+
+    def log_probe(self, x):
+        x = _f64(x).reshape(-1)
+        out = np.zeros_like(x)
+        self._chk(lib().kml_log_probe(self._h, _p(x), x.shape[0], _p(out)), "kml_log_probe")
         return out
 
     def math_probe(self, x):

@@ -70,8 +70,9 @@ __global__ __launch_bounds__(T) void bp_kernel(DevCode c, BpLaunch a, unsigned i
   }
 
   for (;;) {
-    const int cw = dequeue<T>(queue, red);
-    if (cw >= a.B) break;
+    const int entry = dequeue<T>(queue, red);
+    if (entry >= a.B) break;
+    const int cw = a.cw_idx ? a.cw_idx[entry] : entry;
     const double *p0 = a.p0 + (long long)cw * a.p0_stride;
     if (a.p0_sel) p0 += (long long)a.p0_sel[cw] * a.p0_sel_stride;
 
@@ -235,6 +236,7 @@ __global__ __launch_bounds__(T) void bp_kernel(DevCode c, BpLaunch a, unsigned i
       if (a.ret) a.ret[cw] = iter + (iter < a.max_iter);  // :277
       if (a.parity_cnt) a.parity_cnt[cw] = red[0];
       if (a.cw_err && a.ref_bits) a.cw_err[cw] = a.iter_count > 0 ? red[1] : 0;
+      if (a.iters) a.iters[cw] = iter;
       if (a.counters) {
         const unsigned long long vn = conv ? (unsigned long long)iter + 1 : (unsigned long long)iter;
         atomicAdd(&a.counters[CNT_VN_PHASES], vn);

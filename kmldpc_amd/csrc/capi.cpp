@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -76,10 +77,17 @@ struct kml_ctx {
   long long gslots_cap = 0;
   // workspaces
   DBuf w_y, w_h, w_h4, w_hhat, w_p0, w_uu, w_uh, w_uh4, w_ret, w_cch, w_syn, w_sel, w_met, w_pc, w_cnt, w_km, w_cwerr;
+  // soft syndrome metric: candidate / final syndromes, iteration counts, sums, decode lists
+  DBuf s_synm, s_synf, s_itm, s_itf, s_Lm, s_Lf, s_list, s_sel;
+  // Sum of log(syndrom_soft) of the most recent decode that ran a CN phase on
+  // this context (the reference codec's stale member array, reduced to what
+  // the metric reads); -inf = the never-written (zero) array.
+  double soft_state = -INFINITY;
   // resident simulation frames
   DBuf s_uu, s_cc, s_y, s_h;
   int sim_B = 0;
   double sim_snr = 0;
+  uint64_t sim_first = 0;
   // profiling
   bool prof = false;
   std::vector<Pending> pend;
@@ -278,9 +286,11 @@ void drain_profile(kml_ctx *c) {
 }
 
 // Launch BP over n entries with a fresh counter slot; returns the slot.
-int run_bp(kml_ctx *c, kml::BpLaunch a, int &slot_out) {
-  const int slot = next_slot(c);
-  HIPCHK(c, hipMemsetAsync(slot_ptr(c, slot), 0, sizeof(unsigned long long) * kml::CNT_N, c->stream), "memset");
+// reuse >= 0 accumulates into that (already zeroed) slot.
+int run_bp(kml_ctx *c, kml::BpLaunch a, int &slot_out, int reuse = -1) {
+  const int slot = reuse >= 0 ? reuse : next_slot(c);
+  if (reuse < 0)
+    HIPCHK(c, hipMemsetAsync(slot_ptr(c, slot), 0, sizeof(unsigned long long) * kml::CNT_N, c->stream), "memset");
   a.counters = slot_ptr(c, slot);
   a.gslots = c->d_gslots.as<double2>();
   a.gslots_cap = c->gslots_cap;
@@ -362,7 +372,15 @@ struct RecvIO {
   // candidate's metric decode (5G metric), or all zeros for the hard PEG metric
   // (the reference's uu_hat buffer is uninitialised there).
   bool histogram = false;
+  // soft metric stale-state rule: in the simulator (sim) the reference's codec
+  // is copied per task of thread_block_number codewords, so the state restarts
+  // at global indices that are multiples of it (and at the batch start);
+  // kml_decode_frames carries it across calls like one KmCodec instance.
+  bool sim = false;
+  uint64_t first_cw = 0;
 };
+
+int soft_receive(kml_ctx *c, const RecvIO &io, double var, int B, const double2 *hc, int nc, int &bp_slot);
 
 int receive(kml_ctx *c, const RecvIO &io, double snr, int B, int &bp_slot) {
   double var, sigma, ns;
@@ -424,8 +442,7 @@ int receive(kml_ctx *c, const RecvIO &io, double snr, int B, int &bp_slot) {
     HIPCHK(c, c->w_met.ensure(sizeof(double) * 4 * B), "hipMalloc(met)");
     met = c->w_met.as<double>();
   }
-  if (c->rc.metric_soft)
-    return fail(c, KML_E_UNSUP, "[xcodec] metric_type = true (soft syndrome metric) is not implemented yet");
+  if (c->rc.metric_soft) return soft_receive(c, io, var, B, hc, nc, bp_slot);
   // histogram mode: the counters go to a fresh arena slot (read back like BP's)
   unsigned long long *hist_cnt = nullptr;
   if (io.histogram) {
@@ -496,6 +513,193 @@ int receive(kml_ctx *c, const RecvIO &io, double snr, int B, int &bp_slot) {
   return run_bp(c, a, bp_slot);
 }
 
+// Soft syndrome metric (kmcodec.cc:145-156 with metric_type = true): for each
+// candidate, BP for metric_iter iterations, metric = |sum_j log(syndrom_soft[j])|.
+// syndrom_soft is the codec's member array and is only rewritten when a CN
+// phase runs, so a candidate whose decode stops at iteration 0 reads the array
+// left by the most recent decode that did run one — an earlier candidate, the
+// previous codeword's final decode, ... — a sequential dependency across the
+// batch.  Only the sum of logs of that array matters, so the state is one
+// scalar.  The candidates' decodes and sums run batched on the GPU; the host
+// walks the codewords in order resolving the stale reads; a codeword's final
+// decode can be skipped in that walk whenever it provably repeats its chosen
+// candidate's metric decode (same trajectory up to the shorter iteration cap),
+// and otherwise the walk stops at the first codeword whose choice needs it,
+// decodes what is resolved so far, and resumes (one extra round per such link).
+int soft_receive(kml_ctx *c, const RecvIO &io, double var, int B, const double2 *hc, int nc, int &bp_slot) {
+  const int S = c->code.cc_len / c->modem.bits;
+  const size_t cc = (size_t)c->code.cc_len;
+  const int K = c->code.K, M = c->code.M;
+  const int mit = c->rc.metric_iter, max_iter = c->rc.max_iter;
+  const double *cons = c->d_cons.as<double>();
+  const size_t nB = (size_t)nc * B;
+  HIPCHK(c, c->w_p0.ensure(sizeof(double) * cc * nB), "hipMalloc(p0)");
+  HIPCHK(c, c->s_synm.ensure(sizeof(double) * (size_t)M * nB), "hipMalloc(syn)");
+  HIPCHK(c, c->s_itm.ensure(sizeof(int32_t) * nB), "hipMalloc(iters)");
+  HIPCHK(c, c->s_Lm.ensure(sizeof(double) * nB), "hipMalloc(L)");
+  {
+    Timer t(c, "demap", -1, (double)nB * S * (16.0 + 8.0 * c->modem.bits));
+    HIPCHK(c, kml::launch_demap(c->modem.bits, cons, io.y, S, nc, hc, 1, nullptr, var, (int)nB, c->w_p0.as<double>(),
+                                c->stream),
+           "demap candidates");
+    t.stop();
+  }
+  kml::BpLaunch m;
+  m.B = (int)nB;
+  m.iter_count = mit;
+  m.max_iter = max_iter;
+  m.p0 = c->w_p0.as<double>();
+  m.p0_stride = (long long)cc;
+  m.syn = c->s_synm.as<double>();
+  m.iters = c->s_itm.as<int32_t>();
+  if (io.histogram) {
+    HIPCHK(c, c->w_uh4.ensure(nB * K), "hipMalloc(uh4)");
+    m.uu_hat = c->w_uh4.as<uint8_t>();
+  }
+  int mslot = 0;
+  TRY(run_bp(c, m, mslot));
+  {
+    Timer t(c, "metric", -1, (double)nB * M * 8.0);
+    HIPCHK(c, kml::launch_soft_sum(m.syn, M, m.iters, nullptr, (int)nB, c->s_Lm.as<double>(), c->stream), "soft sum");
+    t.stop();
+  }
+  std::vector<int32_t> itm(nB);
+  std::vector<double> Lm(nB);
+  HIPCHK(c, hipMemcpyAsync(itm.data(), m.iters, sizeof(int32_t) * nB, hipMemcpyDeviceToHost, c->stream), "D2H");
+  HIPCHK(c, hipMemcpyAsync(Lm.data(), c->s_Lm.p, sizeof(double) * nB, hipMemcpyDeviceToHost, c->stream), "D2H");
+  TRY(sync(c));
+
+  const long long T = std::max<long long>(1, c->rc.thread_num_blk);
+  auto reset_at = [&](int b) { return io.sim && (b == 0 || (long long)((io.first_cw + (uint64_t)b) % (uint64_t)T) == 0); };
+  double state = io.sim ? -INFINITY : c->soft_state;
+  std::vector<int32_t> chosen(B, 0);
+  std::vector<double> met((size_t)4 * B, 0.0);
+  // candidates of codeword b against the incoming state; returns the state after them
+  auto metrics_of = [&](int b, double in) {
+    double cur = in;
+    for (int i = 0; i < nc; i++) {
+      const size_t e = (size_t)b * nc + i;
+      if (itm[e] > 0) cur = Lm[e];
+      met[(size_t)b * 4 + i] = std::fabs(cur);
+    }
+    int best = 0;
+    for (int i = 1; i < nc; i++)
+      if (met[(size_t)b * 4 + i] < met[(size_t)b * 4 + best]) best = i;
+    chosen[b] = best;
+    return cur;
+  };
+
+  int32_t *d_chosen = io.chosen;
+  if (!d_chosen) {
+    HIPCHK(c, c->s_sel.ensure(sizeof(int32_t) * B), "hipMalloc(sel)");
+    d_chosen = c->s_sel.as<int32_t>();
+  }
+  double *d_met = io.met;
+  if (!d_met) {
+    HIPCHK(c, c->w_met.ensure(sizeof(double) * 4 * B), "hipMalloc(met)");
+    d_met = c->w_met.as<double>();
+  }
+
+  if (io.histogram) {  // GetHistogramData: metric decodes only
+    for (int b = 0; b < B; b++) {
+      if (reset_at(b)) state = -INFINITY;
+      state = metrics_of(b, state);
+    }
+    if (!io.sim) c->soft_state = state;
+    HIPCHK(c, hipMemcpyAsync(d_chosen, chosen.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice, c->stream), "H2D");
+    HIPCHK(c, hipMemcpyAsync(d_met, met.data(), sizeof(double) * 4 * B, hipMemcpyHostToDevice, c->stream), "H2D");
+    bp_slot = next_slot(c);
+    unsigned long long *cnt = slot_ptr(c, bp_slot);
+    HIPCHK(c, hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * kml::CNT_N, c->stream), "memset");
+    const uint8_t *last = c->w_uh4.as<uint8_t>() + (size_t)(nc - 1) * K;
+    if (io.ref_bits)
+      HIPCHK(c, kml::launch_count_packed(io.ref_bits, c->code.Kw, K, last, (long long)nc * K, B, io.cw_err, cnt,
+                                         c->stream),
+             "count");
+    if (io.uh)
+      HIPCHK(c, hipMemcpy2DAsync(io.uh, K, last, (size_t)nc * K, K, B, hipMemcpyDeviceToDevice, c->stream), "copy uh");
+    return sync(c);
+  }
+
+  // final decodes, in rounds
+  HIPCHK(c, c->s_synf.ensure(sizeof(double) * (size_t)M * B), "hipMalloc(syn final)");
+  HIPCHK(c, c->s_itf.ensure(sizeof(int32_t) * B), "hipMalloc(iters final)");
+  HIPCHK(c, c->s_Lf.ensure(sizeof(double) * B), "hipMalloc(L final)");
+  HIPCHK(c, c->s_list.ensure(sizeof(int32_t) * B), "hipMalloc(list)");
+  kml::BpLaunch a;
+  a.iter_count = max_iter;
+  a.max_iter = max_iter;
+  a.uu_hat = io.uh;
+  a.ret = io.ret;
+  a.ref_bits = io.ref_bits;
+  a.cw_err = io.cw_err;
+  a.p0 = c->w_p0.as<double>();
+  a.p0_stride = (long long)cc * nc;
+  a.p0_sel = d_chosen;
+  a.p0_sel_stride = (long long)cc;
+  a.syn = c->s_synf.as<double>();
+  a.iters = c->s_itf.as<int32_t>();
+  a.cw_idx = c->s_list.as<int32_t>();
+  bp_slot = next_slot(c);
+  HIPCHK(c, hipMemsetAsync(slot_ptr(c, bp_slot), 0, sizeof(unsigned long long) * kml::CNT_N, c->stream), "memset");
+  std::vector<int32_t> list;
+  list.reserve(B);
+  int cursor = 0;
+  while (cursor < B) {
+    const size_t first = list.size();
+    bool unknown = false;
+    int pend = -1;
+    double pend_cur = 0.0;
+    int b = cursor;
+    for (; b < B; b++) {
+      if (reset_at(b)) {
+        state = -INFINITY;
+        unknown = false;
+      }
+      const bool stale_first = itm[(size_t)b * nc] <= 0;
+      if (stale_first && unknown) break;  // needs the pending final decode
+      const double cur = metrics_of(b, unknown ? 0.0 : state);
+      list.push_back(b);
+      const int mc = itm[(size_t)b * nc + chosen[b]];
+      // the final decode repeats the chosen candidate's metric decode when
+      // both stop at the same iteration: converged before both caps, or equal caps
+      const bool same = (mc < mit && mc <= max_iter) || mit == max_iter;
+      if (same) {
+        state = mc > 0 ? Lm[(size_t)b * nc + chosen[b]] : cur;
+        unknown = false;
+      } else {
+        unknown = true;
+        pend = b;
+        pend_cur = cur;
+      }
+    }
+    const int n = (int)(list.size() - first);
+    HIPCHK(c, hipMemcpyAsync(d_chosen, chosen.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice, c->stream), "H2D");
+    HIPCHK(c, hipMemcpyAsync(c->s_list.as<int32_t>() + first, list.data() + first, sizeof(int32_t) * n,
+                             hipMemcpyHostToDevice, c->stream),
+           "H2D list");
+    a.B = n;
+    a.cw_idx = c->s_list.as<int32_t>() + first;
+    int slot = 0;
+    TRY(run_bp(c, a, slot, bp_slot));
+    if (unknown && pend >= 0) {  // the last codeword's final decode sets the state
+      const int32_t *pl = c->s_list.as<int32_t>() + first + (n - 1);
+      HIPCHK(c, kml::launch_soft_sum(a.syn, M, a.iters, pl, 1, c->s_Lf.as<double>(), c->stream), "soft sum");
+      int32_t itf = 0;
+      double Lf = 0.0;
+      HIPCHK(c, hipMemcpyAsync(&itf, a.iters + pend, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream), "D2H");
+      HIPCHK(c, hipMemcpyAsync(&Lf, c->s_Lf.as<double>() + pend, sizeof(double), hipMemcpyDeviceToHost, c->stream),
+             "D2H");
+      TRY(sync(c));
+      state = itf > 0 ? Lf : pend_cur;
+    }
+    cursor = b;
+  }
+  if (!io.sim) c->soft_state = state;
+  HIPCHK(c, hipMemcpyAsync(d_met, met.data(), sizeof(double) * 4 * B, hipMemcpyHostToDevice, c->stream), "H2D");
+  return sync(c);
+}
+
 }  // namespace
 
 extern "C" {
@@ -543,7 +747,7 @@ void kml_destroy(kml_ctx *c) {
     drain_profile(c);
     for (DBuf *b : {&c->d_graph, &c->d_cons, &c->d_arena, &c->d_queue, &c->d_gslots, &c->w_y, &c->w_h, &c->w_h4,
                     &c->w_hhat, &c->w_p0, &c->w_uu, &c->w_uh, &c->w_uh4, &c->w_cwerr, &c->w_ret, &c->w_cch, &c->w_syn, &c->w_sel, &c->w_met,
-                    &c->w_pc, &c->w_cnt, &c->w_km, &c->s_uu, &c->s_cc, &c->s_y, &c->s_h})
+                    &c->w_pc, &c->w_cnt, &c->w_km, &c->s_synm, &c->s_synf, &c->s_itm, &c->s_itf, &c->s_Lm, &c->s_Lf, &c->s_list, &c->s_sel, &c->s_uu, &c->s_cc, &c->s_y, &c->s_h})
       b->release();
     hipStreamDestroy(c->stream);
   }
@@ -712,18 +916,27 @@ int kml_decode_frames(kml_ctx *c, const double *y, const double *true_h, double 
   io.met = d_met;
   io.ret = d_ret;
   io.hhat = reinterpret_cast<double2 *>(d_hh);
+  io.histogram = (flags & KML_HISTOGRAM) != 0;
   TRY(receive(c, io, snr, B, slot));
-  if (true_h) {  // single candidate: chosen = 0, metrics unset (kmcodec.cc:66-67)
+  if (true_h && !io.histogram) {  // single candidate: chosen = 0, metrics unset (kmcodec.cc:66-67)
     if (chosen && !(flags & KML_DEVICE_PTRS)) memset(chosen, 0, sizeof(int32_t) * B);
     if (metrics && !(flags & KML_DEVICE_PTRS)) memset(metrics, 0, sizeof(double) * 4 * B);
     if (h_hat && !(flags & KML_DEVICE_PTRS)) memset(h_hat, 0, sizeof(double) * 2 * B);
   } else {
     TRY(copy_out(c, chosen, d_ch, (size_t)B, flags));
     TRY(copy_out(c, metrics, d_met, (size_t)B * 4, flags));
-    TRY(copy_out(c, h_hat, d_hh, (size_t)B * 2, flags));
+    if (true_h) {
+      if (h_hat && !(flags & KML_DEVICE_PTRS)) memset(h_hat, 0, sizeof(double) * 2 * B);
+    } else {
+      TRY(copy_out(c, h_hat, d_hh, (size_t)B * 2, flags));
+    }
   }
   TRY(copy_out(c, uu_hat, d_uh, (size_t)B * c->code.K, flags));
-  TRY(copy_out(c, ret, d_ret, (size_t)B, flags));
+  if (io.histogram) {  // no final decode: no BP return value
+    if (ret && !(flags & KML_DEVICE_PTRS)) memset(ret, 0, sizeof(int32_t) * B);
+  } else {
+    TRY(copy_out(c, ret, d_ret, (size_t)B, flags));
+  }
   return sync(c);
 }
 
@@ -773,6 +986,7 @@ int kml_sim_generate(kml_ctx *c, double snr, uint64_t seed, uint64_t first_cw, i
   t.stop();
   c->sim_B = B;
   c->sim_snr = snr;
+  c->sim_first = first_cw;
   return sync(c);
 }
 
@@ -785,6 +999,8 @@ int sim_receive(kml_ctx *c, double snr, int blind, bool histogram, int &slot) {
   HIPCHK(c, c->w_cwerr.ensure(sizeof(int32_t) * (size_t)c->sim_B), "hipMalloc(cw_err)");
   io.cw_err = c->w_cwerr.as<int32_t>();
   io.histogram = histogram;
+  io.sim = true;
+  io.first_cw = c->sim_first;
   if (histogram) {
     HIPCHK(c, c->w_met.ensure(sizeof(double) * 4 * (size_t)c->sim_B), "hipMalloc(met)");
     io.met = c->w_met.as<double>();
@@ -920,6 +1136,18 @@ int kml_prof_read(kml_ctx *c, const char *stage, int64_t *launches, double *tota
   if (total_ms) *total_ms = s.ms;
   if (alg_bytes) *alg_bytes = s.bytes;
   return KML_OK;
+}
+
+int kml_log_probe(kml_ctx *c, const double *in, int n, double *out) {
+  if (!c || !in || !out || n < 0) return KML_E_ARG;
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const double *d_in;
+  TRY(stage_in(c, c->w_y, in, (size_t)n, 0, d_in));
+  HIPCHK(c, c->w_p0.ensure(sizeof(double) * (size_t)n), "hipMalloc");
+  HIPCHK(c, kml::launch_log_probe(d_in, n, c->w_p0.as<double>(), c->stream), "probe");
+  TRY(copy_out(c, out, (const double *)c->w_p0.as<double>(), (size_t)n, 0));
+  return sync(c);
 }
 
 int kml_math_probe(kml_ctx *c, const double *in, int n, double *out) {

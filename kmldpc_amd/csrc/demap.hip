@@ -214,7 +214,40 @@ __global__ void count_bytes_kernel(const uint8_t *__restrict__ uu, const uint8_t
   }
 }
 
+// KmCodec::Metric, soft branch (src/kmcodec.cc:150-156): L = sum_{j<M} log(syn[j])
+// accumulated in row order from 0.0 like the reference's loop, with the
+// glibc-exact log.  One wave per entry (list[i] or i); entries whose decode ran
+// no CN phase (iters == 0) keep their L (the caller resolves them as stale).
+__global__ __launch_bounds__(64) void soft_sum_kernel(const double *__restrict__ syn, int M,
+                                                      const int32_t *__restrict__ iters,
+                                                      const int32_t *__restrict__ list, double *__restrict__ L) {
+  extern __shared__ double lg[];
+  const int e = list ? list[blockIdx.x] : (int)blockIdx.x;
+  if (iters && iters[e] == 0) return;
+  const double *s = syn + (long long)e * M;
+  for (int j = threadIdx.x; j < M; j += 64) lg[j] = kml_log(s[j]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double acc = 0.0;
+    for (int j = 0; j < M; ++j) acc += lg[j];
+    L[e] = acc;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_soft_sum(const double *syn, int M, const int32_t *iters, const int32_t *list, int n, double *L,
+                           hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const size_t lds = sizeof(double) * (size_t)M;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void *)soft_sum_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(soft_sum_kernel, dim3(n), dim3(64), lds, s, syn, M, iters, list, L);
+  return hipGetLastError();
+}
 
 hipError_t launch_demap(int bits, const double *cons, const double2 *y, int S, int reps, const double2 *h,
                         int h_stride, const int32_t *h_sel, double var, int B, double *p0, hipStream_t s) {

@@ -55,6 +55,10 @@ struct BpLaunch {
   const uint64_t *ref_bits = nullptr;  // [B][Kw] for error counting
   unsigned long long *counters = nullptr;  // [CNT_N]
   int32_t *cw_err = nullptr;     // [B] error bits per codeword vs ref_bits (stop-rule prefix)
+  int32_t *iters = nullptr;      // [B] CN phases run (= iter of the reference loop)
+  // Entry e of the launch decodes codeword cw_idx[e] (NULL: e); every
+  // per-codeword array above is indexed by the codeword, B counts entries.
+  const int32_t *cw_idx = nullptr;
   double2 *gslots = nullptr;     // global slot scratch when E*16 exceeds LDS
   long long gslots_cap = 0;      // number of double2 available
   unsigned int *queue = nullptr; // 4-byte device dequeue counter (zeroed by the launcher)
@@ -89,6 +93,10 @@ hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, co
 // argmin over a [B][nc] parity-count table (first minimum) for the BP-based
 // metrics; metrics[b][4] = |count|.
 hipError_t launch_select(const int32_t *parity_cnt, int nc, int B, double *metrics, int32_t *chosen, hipStream_t s);
+// Soft syndrome metric sums: L[e] = sum_j log(syn[e][j]) in row order, for
+// e = list[i] (or i), i < n; skipped where iters[e] == 0.
+hipError_t launch_soft_sum(const double *syn, int M, const int32_t *iters, const int32_t *list, int n, double *L,
+                           hipStream_t s);
 // CntErr of byte decisions (uh == NULL: all-zero decisions) against packed
 // reference bits; optional per-codeword error bits.
 hipError_t launch_count_packed(const uint64_t *ref, int Kw, int K, const uint8_t *uh, long long uh_stride, int B,
@@ -122,6 +130,7 @@ hipError_t launch_count_bytes(const uint8_t *uu, const uint8_t *uu_hat, int K, i
 
 // Device-side self tests of the exact-math helpers (hypot, complex division).
 hipError_t launch_math_probe(const double *in, int n, double *out, hipStream_t s);
+hipError_t launch_log_probe(const double *in, int n, double *out, hipStream_t s);
 // Device-side self test of the shared-reciprocal division (bp_common.hpp):
 // in[n][3] = (n0, n1, s) -> out[n][4] = (fast q0, fast q1, IEEE q0, IEEE q1).
 hipError_t launch_div_probe(const double *in, int n, double *out, hipStream_t s);

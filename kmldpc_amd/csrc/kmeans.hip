@@ -291,6 +291,11 @@ __global__ void math_probe_kernel(const double *in, int n, double *out) {
   out[4 * i + 3] = kml_exp(a);
 }
 
+__global__ void log_probe_kernel(const double *in, int n, double *out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = kml_log(in[i]);
+}
+
 __global__ void div_probe_kernel(const double *in, int n, double *out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -308,6 +313,12 @@ __global__ void div_probe_kernel(const double *in, int n, double *out) {
 hipError_t launch_div_probe(const double *in, int n, double *out, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(div_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_log_probe(const double *in, int n, double *out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(log_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, out);
   return hipGetLastError();
 }
 

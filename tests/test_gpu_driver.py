@@ -136,3 +136,24 @@ def test_driver_executable_and_python_driver_agree(data_dir, tmp_path):
     assert finals["2.000"][0] <= 1000
     i = m1.index("BER Result")
     assert re.match(r"^1\.000 0\.\d{14}$", m1[i + 1]) and m1[i + 3] == "FER Result"
+
+
+def test_soft_metric_sim_path_statistics(data_dir, tmp_path):
+    """The soft-metric blind path on GPU frames (sim path, per-task stale-state
+    restarts) has the reference's FER within Monte-Carlo confidence (reference:
+    the Decoder-only soft stream of tests/golden/soft, 300 cw)."""
+    from conftest import load_soft_case
+    hdr, z = load_soft_case("peg2304_qpsk_soft")
+    ref = float(np.mean(z["errs"] > 0))
+    cfg = str(tmp_path / "c.toml")
+    write_config(cfg, data_dir, hdr["matrix"], hdr["modem"], known=False, snr=hdr["snr"], metric_type=True,
+                 metric_iter=hdr["metric_iter"], thread_blocks=100000)
+    ctx = K.Context(cfg, data_dir=data_dir, device=0)
+    B = 4000
+    ctx.sim_generate(hdr["snr"], B, seed=31)
+    errs, met, c = ctx.sim_decode_ex(hdr["snr"], blind=True)
+    fer = c["err_blk"] / c["tot_blk"]
+    sigma = np.sqrt(ref * (1 - ref) / len(z["errs"]) + ref * (1 - ref) / B)
+    print(f"soft-metric GPU FER {fer:.4f} vs reference {ref:.4f} (sigma {sigma:.4f})")
+    assert abs(fer - ref) < 4 * sigma
+    ctx.close()

@@ -74,6 +74,24 @@ def test_device_exact_math_matches_host(data_dir):
     assert np.array_equal(out[:20000, 1:3], q)
 
 
+def test_device_log_vs_glibc(data_dir):
+    """The soft metric's log (kml_log) equals glibc's log bit for bit on device:
+    probabilities, the close-to-1 branch, every exponent, special values."""
+    import math
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    rng = np.random.default_rng(3)
+    n = 300000
+    x = np.concatenate([2.0 ** rng.uniform(-45, 0, n // 3), 1.0 + rng.uniform(-0.0625, 0.0647, n // 3),
+                        2.0 ** rng.uniform(-1074, 1023, n // 3),
+                        np.array([0.0, -0.0, 1.0, np.inf, -1.0, np.nan, 5e-324, 1e-12, 1 - 1e-12])])
+    out = ctx.log_probe(x)
+    with np.errstate(all="ignore"):
+        ref = np.array([math.log(v) if v > 0 else (-np.inf if v == 0 else np.nan) for v in x])
+    ref[x == np.inf] = np.inf
+    same = (out.view(np.int64) == ref.view(np.int64)) | (np.isnan(out) & np.isnan(ref))
+    assert same.all(), x[~same][:5]
+
+
 def test_device_exp_vs_glibc(data_dir):
     """The demapper's exp (kml_exp) equals glibc's exp bit for bit on device."""
     import math
@@ -338,3 +356,62 @@ def test_extreme_inputs_match_oracle(data_dir):
         assert r["ret"][i] == ret
         assert np.array_equal(r["cc_hat"][i], cch)
         assert np.array_equal(r["syn"][i], syn, equal_nan=True)
+
+
+# ---------------------------------------------------------------- soft metric
+from conftest import load_soft_case, soft_case_names  # noqa: E402
+
+
+def _soft_setup(case, data_dir):
+    hdr, z = load_soft_case(case)
+    code = O.Code(os.path.join(data_dir, hdr["matrix"]), bool(hdr["is5g"]), True, False, hdr["max_iter"])
+    modem = O.Modem(os.path.join(data_dir, hdr["modem"]))
+    n = len(z["chosen"])
+    uu, cc, th, y = O.gen_frames(code, modem, hdr["snr"], n)
+    for i in range(n):
+        assert crc(y[i]) == z["crc_y"][i]
+    uh = np.unpackbits(z["uu_hat_bits"], axis=1)[:, :hdr["K"]]
+    return hdr, z, y, uh
+
+
+def _soft_ctx(hdr, data_dir):
+    return K.Context(matrix_file=os.path.join(data_dir, hdr["matrix"]), modem_file=os.path.join(data_dir, hdr["modem"]),
+                     is5g=bool(hdr["is5g"]), max_iter=hdr["max_iter"], metric_soft=True,
+                     metric_iter=hdr["metric_iter"], device=0)
+
+
+@pytest.mark.parametrize("case", [c for c in soft_case_names() if not c.endswith("softhist")])
+def test_soft_metric_decode_matches_reference_stream(case, data_dir):
+    """KmCodec::Decoder with metric_type = true over the reference's stream: the
+    chosen candidate, the metrics and uu_hat bit-exact, including the stale
+    syndrom_soft reads, whether the stream is decoded in one batch or split
+    across calls (the context carries the codec state like one instance)."""
+    hdr, z, y, uh = _soft_setup(case, data_dir)
+    n = len(z["chosen"])
+    ctx = _soft_ctx(hdr, data_dir)
+    out = ctx.decode_frames(y, hdr["snr"])
+    assert np.array_equal(out["chosen"], z["chosen"])
+    assert np.array_equal(out["uu_hat"], uh)
+    ref = z["metrics"]
+    assert np.allclose(out["metrics"], ref, rtol=0, atol=6e-15 * np.maximum(1, np.abs(ref)))
+    ctx.close()
+    ctx = _soft_ctx(hdr, data_dir)
+    cut = n // 3 + 1
+    o1 = ctx.decode_frames(y[:cut], hdr["snr"])
+    o2 = ctx.decode_frames(y[cut:], hdr["snr"])
+    assert np.array_equal(np.concatenate([o1["chosen"], o2["chosen"]]), z["chosen"])
+    assert np.array_equal(np.concatenate([o1["uu_hat"], o2["uu_hat"]]), uh)
+    assert np.array_equal(np.concatenate([o1["metrics"], o2["metrics"]]), out["metrics"])
+    ctx.close()
+
+
+def test_soft_metric_histogram_matches_reference(data_dir):
+    """GetHistogramData with the soft metric (histogram mode, no final decode):
+    metrics exact, uu_hat = what the last candidate's metric decode left."""
+    hdr, z, y, uh = _soft_setup("peg2304_qpsk_softhist", data_dir)
+    ctx = _soft_ctx(hdr, data_dir)
+    out = ctx.decode_frames(y, hdr["snr"], histogram=True)
+    assert np.array_equal(out["metrics"], z["metrics"])
+    assert np.array_equal(out["chosen"], z["chosen"])
+    assert np.array_equal(out["uu_hat"], uh)
+    ctx.close()
