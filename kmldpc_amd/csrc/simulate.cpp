@@ -121,5 +121,15 @@ extern "C" int kml_sim_point(kml_ctx *ctx, const kml_point_cfg *cfg, uint64_t se
   kml_dims(ctx, d);
   c.K = d[KML_DIM_K];
   c.ncand = n[3] ? 1 : 4;
+  // soft metric: the reference restarts the codec (and its stale syndrome
+  // state) every thread_block_number codewords; batches that start on those
+  // boundaries keep every stale chain inside one batch of one rank
+  const long long T = n[2];
+  if (n[5] && T > 0) {
+    if (T <= c.batch)
+      c.batch -= (int)(c.batch % T);
+    else if (T <= (1 << 20))
+      c.batch = (int)T;
+  }
   return kml_sweep_point(&c, gpu_batch, &g, reduce, ruser, report, puser, counters);
 }
