@@ -8,7 +8,7 @@ ARCH     ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result -Wno-unused-value
 CSRC     := kmldpc_amd/csrc
 OBJDIR   := build/obj
-CPP_SRCS := config code modem layout capi simulate
+CPP_SRCS := config code modem layout capi simulate refstream
 HIP_SRCS := bp bp_static bp_regular demap kmeans framegen
 OBJS     := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(CPP_SRCS) $(HIP_SRCS)))
 HDRS     := $(wildcard $(CSRC)/*.hpp) include/kmldpc_amd.h

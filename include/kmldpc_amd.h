@@ -195,6 +195,22 @@ int kml_sim_point(kml_ctx *ctx, const kml_point_cfg *cfg, uint64_t seed, kml_all
 /* Copy the resident frames out (for checks): uu[B][K] bytes, y[B][S][2], h[B][2]. */
 int kml_sim_frames(kml_ctx *ctx, uint8_t *uu, double *y, double *h);
 
+/* --- the reference's host random sources (parity runs) ------------------ */
+/* lab::CLCRandNum (randnum.cc:4-92): Park-Miller minimal standard with
+ * Schrage's method; *state = 17 is SetSeed(-1).  Normal(): polar method. */
+double kml_lcg_uniform(int64_t *state);
+void kml_lcg_normal(int64_t *state, double *nn, int len);
+/* lab::CWHRandNum (randnum.cc:95-166): Wichmann-Hill; xyz = {13, 37, 91} is SetSeed(-1). */
+double kml_wh_uniform(int32_t *xyz);
+void kml_wh_normal(int32_t *xyz, double *nn, int len);
+/* lab::SourceSink::GetBitStr / GetSymStr (sourcesink.cc:5-19) on a CLCRandNum state. */
+void kml_get_bit_str(int64_t *state, uint8_t *uu, int len);
+void kml_get_sym_str(int64_t *state, int32_t *uu, int qary, int len);
+/* n frames of Simulator::run_blocks' sequential stream (simulator.cc:118-130)
+ * from a CLCRandNum state (advanced in place): uu[n][K] bytes, true_h[n][2],
+ * y[n][S][2].  Host-side; also works on a host-only context. */
+int kml_ref_frames(const kml_ctx *ctx, int64_t *state, double snr, int n, uint8_t *uu, double *true_h, double *y);
+
 /* --- profiling ----------------------------------------------------------- */
 /* When enabled, every kernel launch of the context is bracketed by HIP events
  * on the context's stream.  kml_prof_read returns, for the named stage

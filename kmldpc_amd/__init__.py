@@ -91,6 +91,13 @@ def lib():
         "kml_math_probe": (I, [P, P, I, P]),
         "kml_div_probe": (I, [P, P, I, P]),
         "kml_log_probe": (I, [P, P, I, P]),
+        "kml_lcg_uniform": (D, [P]),
+        "kml_lcg_normal": (None, [P, P, I]),
+        "kml_wh_uniform": (D, [P]),
+        "kml_wh_normal": (None, [P, P, I]),
+        "kml_get_bit_str": (None, [P, P, I]),
+        "kml_get_sym_str": (None, [P, P, I, I]),
+        "kml_ref_frames": (I, [P, P, D, I, P, P, P]),
         "kml_sim_decode_ex": (I, [P, D, I, I, P, P, P]),
         "kml_run_config": (I, [P, P, P]),
         "kml_sweep_point": (I, [C.POINTER(PointCfg), BATCH_FN, P, ALLREDUCE_FN, P, REPORT_FN, P, P]),
@@ -329,6 +336,16 @@ class Context:
         self._chk(lib().kml_div_probe(self._h, _p(x), x.shape[0], _p(out)), "kml_div_probe")
         return out
 
+    def ref_frames(self, rng, snr, n):
+        """n frames of the reference's sequential stream (Simulator::run_blocks)
+        from rng (a CLCRandNum); returns uu[n][K], true_h[n][2], y[n][S][2]."""
+        uu = np.zeros((n, self.K), np.uint8)
+        th = np.zeros((n, 2))
+        y = np.zeros((n, self.S, 2))
+        self._chk(lib().kml_ref_frames(self._h, _p(rng.state), float(snr), int(n), _p(uu), _p(th), _p(y)),
+                  "kml_ref_frames")
+        return uu, th, y
+
     def log_probe(self, x):
         x = _f64(x).reshape(-1)
         out = np.zeros_like(x)
@@ -339,6 +356,49 @@ class Context:
         x = _f64(x).reshape(-1, 4)
         out = np.zeros_like(x)
         self._chk(lib().kml_math_probe(self._h, _p(x), x.shape[0], _p(out)), "kml_math_probe")
+        return out
+
+
+# ---------------------------------------------------------------------------
+# The reference's host random sources (lib/lab/src/randnum.cc, sourcesink.cc)
+
+class CLCRandNum:
+    """lab::CLCRandNum: Park-Miller (A = 48271) + polar normals; SetSeed(-1) -> state 17."""
+
+    def __init__(self, state=17):
+        self.state = np.array([state], np.int64)
+
+    def Uniform(self):
+        return lib().kml_lcg_uniform(_p(self.state))
+
+    def Normal(self, n):
+        out = np.zeros(n)
+        lib().kml_lcg_normal(_p(self.state), _p(out), int(n))
+        return out
+
+    def GetBitStr(self, n):
+        out = np.zeros(n, np.uint8)
+        lib().kml_get_bit_str(_p(self.state), _p(out), int(n))
+        return out
+
+    def GetSymStr(self, qary, n):
+        out = np.zeros(n, np.int32)
+        lib().kml_get_sym_str(_p(self.state), _p(out), int(qary), int(n))
+        return out
+
+
+class CWHRandNum:
+    """lab::CWHRandNum: Wichmann-Hill + polar normals; SetSeed(-1) -> (13, 37, 91)."""
+
+    def __init__(self, xyz=(13, 37, 91)):
+        self.xyz = np.array(xyz, np.int32)
+
+    def Uniform(self):
+        return lib().kml_wh_uniform(_p(self.xyz))
+
+    def Normal(self, n):
+        out = np.zeros(n)
+        lib().kml_wh_normal(_p(self.xyz), _p(out), int(n))
         return out
 
 

@@ -17,6 +17,11 @@
 #include "layout.hpp"
 #include "modem.hpp"
 
+namespace kml {
+int ref_frames(const LdpcCode &code, const Modem &modem, int64_t *state, double snr, int n, uint8_t *uu_out,
+               double *h_out, double *y_out);
+}
+
 namespace {
 
 struct DBuf {
@@ -1136,6 +1141,11 @@ int kml_prof_read(kml_ctx *c, const char *stage, int64_t *launches, double *tota
   if (total_ms) *total_ms = s.ms;
   if (alg_bytes) *alg_bytes = s.bytes;
   return KML_OK;
+}
+
+int kml_ref_frames(const kml_ctx *c, int64_t *state, double snr, int n, uint8_t *uu, double *true_h, double *y) {
+  if (!c || !state || n < 0 || (n > 0 && (!uu || !true_h || !y))) return KML_E_ARG;
+  return kml::ref_frames(c->code, c->modem, state, snr, n, uu, true_h, y);
 }
 
 int kml_log_probe(kml_ctx *c, const double *in, int n, double *out) {

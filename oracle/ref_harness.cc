@@ -46,7 +46,7 @@ static void put_bits(FILE *f, const int *v, int n) {
 int main(int argc, char **argv) {
   if (argc < 5) {
     fprintf(stderr, "usage: %s config.toml snr n_codewords out.bin [mode]\n", argv[0]);
-    fprintf(stderr, "  mode: frames (default) | simulate | soft | softhist\n");
+    fprintf(stderr, "  mode: frames (default) | simulate | soft | softhist | rng\n");
     return 2;
   }
   const std::string cfg = argv[1];
@@ -64,6 +64,31 @@ int main(int argc, char **argv) {
 
   lab::CLCRandNum::Get().SetSeed(-1);
   lab::CWHRandNum::Get().SetSeed(-1);
+
+  if (mode == "rng") {
+    // The host random sources with SetSeed(-1): CLCRandNum / CWHRandNum
+    // uniforms and normals, SourceSink::GetSymStr / GetBitStr.
+    FILE *f = fopen(out_path.c_str(), "wb");
+    if (!f) return 1;
+    const int n = ncw;
+    for (int i = 0; i < n; i++) put_f64(f, lab::CLCRandNum::Get().Uniform());
+    for (int i = 0; i < n; i++) put_f64(f, lab::CWHRandNum::Get().Uniform());
+    std::vector<double> nn(n + 1);
+    lab::CLCRandNum::Get().Normal(nn.data(), n + 1);  // odd length: the single-value tail
+    for (int i = 0; i <= n; i++) put_f64(f, nn[i]);
+    lab::CWHRandNum::Get().Normal(nn.data(), n + 1);
+    for (int i = 0; i <= n; i++) put_f64(f, nn[i]);
+    lab::SourceSink ss;
+    std::vector<int> sym(n), bits(n);
+    ss.GetSymStr(sym.data(), 16, n);
+    for (int i = 0; i < n; i++) put_i32(f, sym[i]);
+    ss.GetSymStr(sym.data(), 3, n);
+    for (int i = 0; i < n; i++) put_i32(f, sym[i]);
+    ss.GetBitStr(bits.data(), n);
+    for (int i = 0; i < n; i++) put_i32(f, bits[i]);
+    fclose(f);
+    return 0;
+  }
 
   std::ifstream ifs(cfg, std::ios_base::binary);
   if (!ifs.is_open()) {

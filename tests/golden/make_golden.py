@@ -203,7 +203,29 @@ def make_soft(tmp):
               f"inf_metrics={int(np.isinf(arrs['metrics']).sum())}")
 
 
+def make_rng(tmp, n=2000):
+    """Reference RNG streams with SetSeed(-1) -> golden/rng.npz."""
+    out = os.path.join(tmp, "rng.bin")
+    subprocess.run([HARNESS, "unused.toml", "0", str(n), out, "rng"], check=True)
+    b = open(out, "rb").read()
+    o = 0
+    arr = {}
+    for key, cnt, dt in [("clc_u", n, "<f8"), ("wh_u", n, "<f8"), ("clc_n", n + 1, "<f8"), ("wh_n", n + 1, "<f8"),
+                         ("sym16", n, "<i4"), ("sym3", n, "<i4"), ("bits", n, "<i4")]:
+        arr[key] = np.frombuffer(b, dtype=dt, count=cnt, offset=o).copy()
+        o += cnt * np.dtype(dt).itemsize
+    np.savez_compressed(os.path.join(HERE, "rng.npz"), **arr)
+    print("rng:", {k: v[:3] for k, v in arr.items()})
+
+
 def main():
+    if "--rng" in sys.argv:
+        tmp = tempfile.mkdtemp()
+        try:
+            make_rng(tmp)
+        finally:
+            shutil.rmtree(tmp)
+        return
     if "--soft" in sys.argv:
         tmp = tempfile.mkdtemp()
         try:

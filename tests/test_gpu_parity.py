@@ -266,15 +266,15 @@ def test_decode_frames_vs_reference_stream(case, data_dir):
 
 
 def test_reference_counters_2000(data_dir):
-    """End-to-end SourceSink counters of the reference (2000 cw, seed 17)."""
+    """End-to-end SourceSink counters of the reference (2000 cw, seed 17),
+    reproduced by the product alone: the reference's frame stream from
+    kml_ref_frames (CLCRandNum state 17), the GPU receive path, CntErr."""
     ctr = json.load(open(os.path.join(GOLDEN, "counters.json")))
     for name, c in ctr.items():
         ctx = ctx_for(data_dir, c["matrix"], c["modem"], c["is5g"], c["max_iter"])
-        oc = oracle_for(data_dir, c["matrix"], c["is5g"], c["max_iter"])
-        om = O.Modem(os.path.join(data_dir, c["modem"]))
-        uu, cc, th, y = O.gen_frames(oc, om, c["snr"], c["n"])
+        uu, th, y = ctx.ref_frames(K.CLCRandNum(17), c["snr"], c["n"])
         r = ctx.decode_frames(y, c["snr"], th if c["known"] else None)
-        cnt = ctx.count_errors(uu.astype(np.uint8), r["uu_hat"])
+        cnt = ctx.count_errors(uu, r["uu_hat"])
         assert (cnt["err_blk"], cnt["err_bit"], cnt["tot_blk"]) == (c["err_blk"], c["err_bit"], c["tot_blk"]), name
 
 

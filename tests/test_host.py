@@ -184,3 +184,37 @@ def test_log_host_restatement(tmp_path):
     out = subprocess.run([str(exe), "2000000"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
     assert "log_fma_mismatch=0" in out.stdout
+
+
+# ---------------------------------------------------------- host random sources
+def test_reference_rngs_match_reference():
+    """CLCRandNum / CWHRandNum / GetSymStr / GetBitStr with SetSeed(-1) equal the
+    reference's streams (tests/golden/rng.npz, from the reference harness)."""
+    z = np.load(os.path.join(REPO, "tests", "golden", "rng.npz"))
+    n = len(z["clc_u"])
+    c = K.CLCRandNum()
+    w = K.CWHRandNum()
+    assert np.array_equal([c.Uniform() for _ in range(n)], z["clc_u"])
+    assert np.array_equal([w.Uniform() for _ in range(n)], z["wh_u"])
+    assert np.array_equal(c.Normal(n + 1), z["clc_n"])
+    assert np.array_equal(w.Normal(n + 1), z["wh_n"])
+    assert np.array_equal(c.GetSymStr(16, n), z["sym16"])
+    assert np.array_equal(c.GetSymStr(3, n), z["sym3"])
+    assert np.array_equal(c.GetBitStr(n), z["bits"].astype(np.uint8))
+
+
+@pytest.mark.parametrize("case", ["peg2304_qpsk_known", "bg2_16qam_known", "peg8064_64qam_known"])
+def test_ref_frames_reproduce_reference_stream(case, data_dir):
+    """kml_ref_frames = the reference's frames for seed 17 (fixture CRCs): the
+    product side of 'identical RNG seeds' parity runs."""
+    import zlib
+    from conftest import load_case
+    hdr, z = load_case(case)
+    ctx = K.Context(matrix_file=os.path.join(data_dir, hdr["matrix"]), modem_file=os.path.join(data_dir, hdr["modem"]),
+                    is5g=bool(hdr["is5g"]), max_iter=hdr["max_iter"], device=-1)
+    n = min(40, len(z["s_crc_y"]))
+    uu, th, y = ctx.ref_frames(K.CLCRandNum(), hdr["snr"], n)
+    for i in range(n):
+        assert zlib.crc32(y[i].tobytes()) & 0xFFFFFFFF == z["s_crc_y"][i]
+        assert zlib.crc32(uu[i].tobytes()) & 0xFFFFFFFF == z["s_crc_uu"][i]
+    assert np.array_equal(th, z["s_true_h"][:n])
