@@ -204,7 +204,7 @@ def make_soft(tmp):
 
 
 def make_rng(tmp, n=2000):
-    """Reference RNG streams with SetSeed(-1) -> golden/rng.npz."""
+    """Reference RNG streams with SetSeed(-1) -> golden/host/rng.npz."""
     out = os.path.join(tmp, "rng.bin")
     subprocess.run([HARNESS, "unused.toml", "0", str(n), out, "rng"], check=True)
     b = open(out, "rb").read()
@@ -214,7 +214,8 @@ def make_rng(tmp, n=2000):
                          ("sym16", n, "<i4"), ("sym3", n, "<i4"), ("bits", n, "<i4")]:
         arr[key] = np.frombuffer(b, dtype=dt, count=cnt, offset=o).copy()
         o += cnt * np.dtype(dt).itemsize
-    np.savez_compressed(os.path.join(HERE, "rng.npz"), **arr)
+    os.makedirs(os.path.join(HERE, "host"), exist_ok=True)
+    np.savez_compressed(os.path.join(HERE, "host", "rng.npz"), **arr)
     print("rng:", {k: v[:3] for k, v in arr.items()})
 
 

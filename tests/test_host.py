@@ -190,7 +190,7 @@ def test_log_host_restatement(tmp_path):
 def test_reference_rngs_match_reference():
     """CLCRandNum / CWHRandNum / GetSymStr / GetBitStr with SetSeed(-1) equal the
     reference's streams (tests/golden/rng.npz, from the reference harness)."""
-    z = np.load(os.path.join(REPO, "tests", "golden", "rng.npz"))
+    z = np.load(os.path.join(REPO, "tests", "golden", "host", "rng.npz"))
     n = len(z["clc_u"])
     c = K.CLCRandNum()
     w = K.CWHRandNum()
