@@ -18,73 +18,12 @@
 // reference's order; exp() is kml_exp, a bit-exact restatement of the glibc exp
 // the reference calls (the ROCm device exp differs from it in the last bit on
 // ~6% of inputs), so P0 is bit-identical to the CPU path.
-#include "exact_math.hpp"
+#include "demap_common.hpp"
 #include "kernels.hpp"
 
 namespace kml {
 
 namespace {
-
-constexpr double kSmallestProb = 1.0e-12;
-
-__device__ __forceinline__ double prob_clip(double v) {  // utility.cc:18-26
-  if (v < kSmallestProb) return kSmallestProb;
-  if (v > 1.0 - kSmallestProb) return 1.0 - kSmallestProb;
-  return v;
-}
-
-// P0 for the MB bits of one symbol.
-template <int MB>
-__device__ __forceinline__ void demap_symbol(const double *__restrict__ cons, double yr, double yi, double hr, double hi,
-                                             double var, double *out) {
-  constexpr int KC = 1 << MB;
-  double pr[KC];
-  double mx = 0.0;
-#pragma unroll
-  for (int k = 0; k < KC; ++k) {
-    const double cr = cons[2 * k], ci = cons[2 * k + 1];
-    double sr = cr * hr - ci * hi;  // symbol *= theta_h
-    double si = cr * hi + ci * hr;
-    sr = sr - yr;  // symbol -= yy
-    si = si - yi;
-    const double d = (sr * sr + si * si) / var;
-    pr[k] = -d;
-    if (k == 0 || mx < pr[k]) mx = pr[k];  // *max_element
-  }
-  double sum = 0.0;
-#pragma unroll
-  for (int k = 0; k < KC; ++k) {
-    pr[k] = kml_exp(pr[k] - mx);  // glibc exp, bit-exact (exact_math.hpp)
-    sum += pr[k];
-  }
-  // normalise + ProbClip (modemlinearsystem.cc:240-246), ProbClip again (modem.cc:27)
-  double w = 1.0;  // prod over bits of bitLin (= 0.5) or 1 - bitLin (= 0.5)
-#pragma unroll
-  for (int j = 0; j < MB; ++j) w *= 0.5;
-  double sum2 = 0.0;
-#pragma unroll
-  for (int k = 0; k < KC; ++k) {
-    pr[k] = prob_clip(prob_clip(pr[k] / sum));
-    pr[k] = w * pr[k];
-    sum2 += pr[k];
-  }
-#pragma unroll
-  for (int k = 0; k < KC; ++k) pr[k] /= sum2;
-#pragma unroll
-  for (int j = 0; j < MB; ++j) {
-    double q0 = 0.0, q1 = 0.0;
-#pragma unroll
-    for (int k = 0; k < KC; ++k) {
-      if (((k >> (MB - 1 - j)) & 1) == 0)
-        q0 += pr[k];
-      else
-        q1 += pr[k];
-    }
-    q0 /= 0.5;
-    q1 /= (1.0 - 0.5);
-    out[j] = prob_clip(q0 / (q0 + q1));
-  }
-}
 
 template <int MB>
 __global__ __launch_bounds__(256) void demap_kernel(const double *__restrict__ cons, const double2 *__restrict__ y,
