@@ -34,6 +34,8 @@
 //              (Smith divisions).
 // km_init (first max of |y|, same screening) and km_final (h_hat and the 4
 // rotated candidates) are lane-per-codeword.
+#include <cstdlib>
+
 #include "bp_common.hpp"
 #include "exact_math.hpp"
 #include "kernels.hpp"
@@ -242,9 +244,221 @@ __global__ void km_final_kernel(const double *__restrict__ cons, const double *_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused k-means: one workgroup per codeword runs the whole KMeans::Run.  The
+// symbols are staged in LDS once; each iteration assigns in parallel (same
+// screening as km_assign, 64-symbol words by ballot), compacts the cluster-0
+// members' values into LDS in ascending symbol order, and two lanes run the
+// re / im accumulation chains in that order (the reference's sequential sum,
+// software-pipelined so the adds, not the LDS latency, set its pace); lane 0
+// then tests convergence and updates h_hat.  One launch instead of two per
+// iteration, and y is read from HBM once.
+constexpr int kFusedT = 256;
+constexpr int kFusedMaxW = 64;  // 64-symbol words: S <= 4096
+
+__device__ __forceinline__ double wave_max(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+
+// acc + x[0] + x[2] + ... + x[2(n-1)] in that order (stride 2: one component
+// of a double2 array).
+__device__ __forceinline__ double ordered_sum(double acc, const double *x, int n) {
+  int i = 0;
+  for (; i + 4 <= n; i += 4) {
+    const double a0 = x[2 * i], a1 = x[2 * i + 2], a2 = x[2 * i + 4], a3 = x[2 * i + 6];
+    acc = acc + a0;
+    acc = acc + a1;
+    acc = acc + a2;
+    acc = acc + a3;
+  }
+  for (; i < n; ++i) acc = acc + x[2 * i];
+  return acc;
+}
+
+template <int KC>
+__global__ __launch_bounds__(kFusedT) void km_fused_kernel(const double *__restrict__ cons,
+                                                           const double *__restrict__ rot,
+                                                           const double2 *__restrict__ y, int S, int iters,
+                                                           double2 *__restrict__ h_hat, double2 *__restrict__ h4) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char kmem[];
+  double2 *ys = reinterpret_cast<double2 *>(kmem);  // [S] symbols
+  double2 *ym = ys + S;                              // [S] compacted cluster-0 members
+  __shared__ double2 cl[KC];
+  __shared__ uint64_t wbits[kFusedMaxW];
+  __shared__ int wpos[kFusedMaxW + 1];
+  __shared__ double red_d[kFusedT / 64];
+  __shared__ int red_i[kFusedT / 64];
+  __shared__ double2 s_hat;
+  __shared__ int s_done, s_exact;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = kFusedT / 64;
+  const int cw = blockIdx.x;
+  const int Sw = (S + 63) / 64;
+  const double2 *yy = y + (long long)cw * S;
+  for (int j = tid; j < S; j += kFusedT) ys[j] = yy[j];
+  if (tid == 0) s_exact = 0;
+  __syncthreads();
+
+  // ---- first max |y| (kmeans.cc:17-22), screened like first_max_abs
+  double best = -1.0;
+  bool ex = false;
+  for (int j = tid; j < S; j += kFusedT) {
+    const double2 v = ys[j];
+    const double d = v.x * v.x + v.y * v.y;
+    if (!d2_ok(d) && !(d == 0.0)) ex = true;
+    if (d > best) best = d;
+  }
+  best = wave_max(best);
+  const bool wex = __ballot(ex) != 0;
+  if (lane == 0) {
+    red_d[wave] = best;
+    if (wex) s_exact = 1;
+  }
+  __syncthreads();
+  best = red_d[0];
+  for (int w = 1; w < NW; ++w) best = fmax(best, red_d[w]);
+  int mi;
+  if (!s_exact && best > 0.0) {
+    double hb = -1.0;  // max exact |y| among the band's candidates
+    for (int j = tid; j < S; j += kFusedT) {
+      const double2 v = ys[j];
+      if (v.x * v.x + v.y * v.y >= best * (1.0 - kTieBand)) hb = fmax(hb, kml_hypot(v.x, v.y));
+    }
+    hb = wave_max(hb);
+    __syncthreads();
+    if (lane == 0) red_d[wave] = hb;
+    __syncthreads();
+    hb = red_d[0];
+    for (int w = 1; w < NW; ++w) hb = fmax(hb, red_d[w]);
+    int jm = 0x7fffffff;  // the first index attaining it
+    for (int j = tid; j < S; j += kFusedT) {
+      const double2 v = ys[j];
+      if (v.x * v.x + v.y * v.y >= best * (1.0 - kTieBand) && kml_hypot(v.x, v.y) == hb) jm = min(jm, j);
+    }
+    jm = wave_min_i(jm);
+    if (lane == 0) red_i[wave] = jm;
+    __syncthreads();
+    mi = red_i[0];
+    for (int w = 1; w < NW; ++w) mi = min(mi, red_i[w]);
+  } else {  // the reference loop, sequentially (non-finite / extreme / all-zero input)
+    if (tid == 0) {
+      int m = 0;
+      double h0 = kml_hypot(ys[0].x, ys[0].y);
+      for (int j = 1; j < S; ++j) {
+        const double h = kml_hypot(ys[j].x, ys[j].y);
+        if (h0 < h) {
+          h0 = h;
+          m = j;
+        }
+      }
+      red_i[0] = m;
+    }
+    __syncthreads();
+    mi = red_i[0];
+  }
+  const cplx c0{cons[0], cons[1]};
+  cplx hat = kml_cdiv(cplx{ys[mi].x, ys[mi].y}, c0);  // kmeans.cc:25
+  cplx prev{0.0, 0.0};
+  bool have_prev = false;
+  double sr = 0.0, si = 0.0;  // cumulative cluster-0 sum (kmeans.cc:33-34, 46)
+  int cnt = 0;
+  for (int it = 0; it < iters; ++it) {
+    for (int k = tid; k < KC; k += kFusedT) {
+      const cplx p = kml_cmul(cplx{cons[2 * k], cons[2 * k + 1]}, hat);  // clusters_[k] = c[k] * hatH
+      cl[k] = make_double2(p.re, p.im);
+    }
+    __syncthreads();
+    // assignment: is cluster 0 the first minimum?  (kmeans.cc:36-46)
+    for (int w = wave; w < Sw; w += NW) {
+      const int j = w * 64 + lane;
+      const bool m = j < S && member0<KC>(cl, ys[j].x, ys[j].y);
+      const uint64_t bits = __ballot(m);
+      if (lane == 0) wbits[w] = bits;
+    }
+    __syncthreads();
+    if (tid < 64) {  // word offsets: exclusive prefix of the popcounts (Sw <= 64)
+      int c = tid < Sw ? __popcll(wbits[tid]) : 0;
+      int x = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(x, o);
+        if (lane >= o) x += t;
+      }
+      wpos[tid] = x - c;
+      if (tid == 63) wpos[kFusedMaxW] = x;
+    }
+    __syncthreads();
+    for (int w = wave; w < Sw; w += NW) {
+      const uint64_t bits = wbits[w];
+      if ((bits >> lane) & 1) ym[wpos[w] + __popcll(bits & ((1ull << lane) - 1))] = ys[w * 64 + lane];
+    }
+    __syncthreads();
+    const int n = wpos[kFusedMaxW];
+    if (tid < 2) {  // lane 0: real chain, lane 1: imaginary chain, ascending j
+      const double acc = ordered_sum(tid == 0 ? sr : si, reinterpret_cast<const double *>(ym) + tid, n);
+      const double other = __shfl_xor(acc, 1);
+      sr = tid == 0 ? acc : other;
+      si = tid == 0 ? other : acc;
+      cnt += n;
+      if (tid == 0) {
+        // convergence: every cluster equals the previous iteration's (kmeans.cc:47-56)
+        bool same = true;
+        for (int k = 0; k < KC && same; ++k) {
+          const cplx ck{cons[2 * k], cons[2 * k + 1]};
+          const cplx a = kml_cmul(ck, hat);
+          const cplx b = have_prev ? kml_cmul(ck, prev) : cplx{0.0, 0.0};
+          same = (a.re == b.re) && (a.im == b.im);
+        }
+        int done = 0;
+        if (same) {
+          done = 1;
+        } else {
+          prev = hat;
+          have_prev = true;
+          const cplx m0 = kml_cdiv(cplx{sr, si}, cplx{(double)cnt, 0.0});  // kmeans.cc:59-62
+          hat = kml_cdiv(m0, c0);                                         // kmeans.cc:64-71
+        }
+        s_hat = make_double2(hat.re, hat.im);
+        s_done = done;
+      }
+    }
+    __syncthreads();
+    hat = cplx{s_hat.x, s_hat.y};
+    if (s_done) break;
+  }
+  if (tid == 0) {
+    const cplx hh = kml_cdiv(kml_cmul(c0, hat), c0);  // simulator.cc:145
+    h_hat[cw] = make_double2(hh.re, hh.im);
+    for (int j = 0; j < 4; ++j) {  // simulator.cc:146-148
+      const cplx r = kml_cmul(hh, cplx{rot[2 * j], rot[2 * j + 1]});
+      h4[(long long)cw * 4 + j] = make_double2(r.re, r.im);
+    }
+  }
+}
+
+template <int KC>
+bool run_kmeans_fused(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
+                      double2 *h_hat, double2 *h4, hipStream_t s, hipError_t &err) {
+  const size_t lds = 2 * sizeof(double2) * (size_t)S;
+  if (S > 64 * kFusedMaxW || lds > 128 * 1024) return false;
+  if (const char *e = getenv("KML_KMEANS"))
+    if (e[0] == 's') return false;  // KML_KMEANS=split: the two-launch form (A/B)
+  err = hipFuncSetAttribute((const void *)km_fused_kernel<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return true;
+  hipLaunchKernelGGL(km_fused_kernel<KC>, dim3(B), dim3(kFusedT), lds, s, cons, rot, y, S, iters, h_hat, h4);
+  err = hipGetLastError();
+  return true;
+}
+
 template <int KC>
 hipError_t run_kmeans(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
                       KmState *st, uint64_t *mem, double2 *h_hat, double2 *h4, hipStream_t s) {
+  hipError_t ferr = hipSuccess;
+  if (run_kmeans_fused<KC>(cons, rot, y, S, iters, B, h_hat, h4, s, ferr)) return ferr;
   const int Sw = (S + 63) / 64;
   const dim3 lanes((B + 63) / 64), l64(64);
   hipLaunchKernelGGL(km_init_kernel, lanes, l64, 0, s, cons, y, S, B, st);
