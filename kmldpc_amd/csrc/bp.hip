@@ -337,6 +337,10 @@ hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const c
     hipError_t e = launch_bp_static(c, a, s);
     if (e != hipErrorNotSupported) return e;
   }
+  if (!lds && variant == 0) {
+    hipError_t e = launch_bp_coop(c, a, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   if (!lds && (a.gslots == nullptr || a.gslots_cap < c.E)) {
     if (err) *err = "global slot workspace missing";
     return hipErrorInvalidValue;

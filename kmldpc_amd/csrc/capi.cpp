@@ -78,8 +78,10 @@ struct kml_ctx {
   double vn_flops = 0, cn_flops = 0;
   DBuf d_arena;  // kArenaSlots x CNT_N counters
   int arena_next = 0;
-  DBuf d_queue, d_gslots;
+  DBuf d_queue, d_gslots, d_gsync, d_gcch;
   long long gslots_cap = 0;
+  int coop_groups = 0;      // cooperative BP groups (0: kernel not used)
+  bool coop_pending = false;  // a cooperative launch whose abort word is unchecked
   // workspaces
   DBuf w_y, w_h, w_h4, w_hhat, w_p0, w_uu, w_uh, w_uh4, w_ret, w_cch, w_syn, w_sel, w_met, w_pc, w_cnt, w_km, w_cwerr;
   // soft syndrome metric: candidate / final syndromes, iteration counts, sums, decode lists
@@ -139,6 +141,10 @@ int upload_code(kml_ctx *c) {
   kml::RegularLayout plan;
   if (reg_T > 0) kml::plan_regular_layout(L, reg_T, plan);
   const std::vector<int32_t> &vn_order = reg_T > 0 ? plan.order : L.vn_order;
+  if (reg_T <= 0) {  // column -> vn position, used by the cooperative kernel
+    plan.pos.assign(L.N, 0);
+    for (int p = 0; p < L.N; p++) plan.pos[L.vn_order[p]] = p;
+  }
   reserve(L.col_slot.size() * 4);
   reserve(vn_order.size() * 4);
   reserve(L.cn_order.size() * 4);
@@ -170,7 +176,7 @@ int upload_code(kml_ctx *c) {
   d.cn_order = reinterpret_cast<const int32_t *>(base + off[5]);
   d.enc_info = reinterpret_cast<const uint64_t *>(base + off[6]);
   d.reg_c2v = reg_T > 0 ? reinterpret_cast<const int32_t *>(base + off[7]) : nullptr;
-  d.reg_pos = reg_T > 0 ? reinterpret_cast<const int32_t *>(base + off[8]) : nullptr;
+  d.reg_pos = reinterpret_cast<const int32_t *>(base + off[8]);
   d.M = L.M;
   d.N = L.N;
   d.E = L.E;
@@ -197,6 +203,11 @@ int upload_code(kml_ctx *c) {
   if (need > 0) {
     HIPCHK(c, c->d_gslots.ensure((size_t)need * sizeof(double2)), "hipMalloc(gslots)");
     c->gslots_cap = need;
+  }
+  c->coop_groups = kml::bp_coop_groups(d);
+  if (c->coop_groups > 0) {
+    HIPCHK(c, c->d_gsync.ensure(kml::bp_coop_sync_bytes(c->coop_groups)), "hipMalloc(gsync)");
+    HIPCHK(c, c->d_gcch.ensure((size_t)c->coop_groups * L.N), "hipMalloc(gcch)");
   }
   return KML_OK;
 }
@@ -300,6 +311,9 @@ int run_bp(kml_ctx *c, kml::BpLaunch a, int &slot_out, int reuse = -1) {
   a.gslots = c->d_gslots.as<double2>();
   a.gslots_cap = c->gslots_cap;
   a.queue = c->d_queue.as<unsigned int>();
+  a.gsync = c->d_gsync.p;
+  a.gcch = c->d_gcch.as<uint8_t>();
+  if (c->coop_groups > 0) c->coop_pending = true;
   Timer t(c, "bp", slot, (double)a.B * 8.0 * c->code.cc_len);
   const char *msg = nullptr;
   hipError_t e = kml::launch_bp(c->dc, a, c->stream, &msg);
@@ -346,6 +360,13 @@ int copy_out(kml_ctx *c, T *dst, const T *dev, size_t n, int flags) {
 
 int sync(kml_ctx *c) {
   HIPCHK(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  if (c->coop_pending) {
+    c->coop_pending = false;
+    kml::BpLaunch a;
+    a.gsync = c->d_gsync.p;
+    if (kml::bp_coop_aborted(a, c->coop_groups, c->stream))
+      return fail(c, KML_E_HIP, "cooperative BP kernel aborted (a group barrier timed out)");
+  }
   return KML_OK;
 }
 
@@ -750,7 +771,7 @@ void kml_destroy(kml_ctx *c) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     drain_profile(c);
-    for (DBuf *b : {&c->d_graph, &c->d_cons, &c->d_arena, &c->d_queue, &c->d_gslots, &c->w_y, &c->w_h, &c->w_h4,
+    for (DBuf *b : {&c->d_graph, &c->d_cons, &c->d_arena, &c->d_queue, &c->d_gslots, &c->d_gsync, &c->d_gcch, &c->w_y, &c->w_h, &c->w_h4,
                     &c->w_hhat, &c->w_p0, &c->w_uu, &c->w_uh, &c->w_uh4, &c->w_cwerr, &c->w_ret, &c->w_cch, &c->w_syn, &c->w_sel, &c->w_met,
                     &c->w_pc, &c->w_cnt, &c->w_km, &c->s_synm, &c->s_synf, &c->s_itm, &c->s_itf, &c->s_Lm, &c->s_Lf, &c->s_list, &c->s_sel, &c->s_uu, &c->s_cc, &c->s_y, &c->s_h})
       b->release();

@@ -59,6 +59,10 @@ struct BpLaunch {
   // Entry e of the launch decodes codeword cw_idx[e] (NULL: e); every
   // per-codeword array above is indexed by the codeword, B counts entries.
   const int32_t *cw_idx = nullptr;
+  // Cooperative global-slot kernel (bp_coop.hip): per-group sync blocks
+  // (bp_coop_sync_bytes) and per-group hard-decision bytes (groups x N).
+  void *gsync = nullptr;
+  uint8_t *gcch = nullptr;
   double2 *gslots = nullptr;     // global slot scratch when E*16 exceeds LDS
   long long gslots_cap = 0;      // number of double2 available
   unsigned int *queue = nullptr; // 4-byte device dequeue counter (zeroed by the launcher)
@@ -69,6 +73,12 @@ struct BpLaunch {
 // fits it, else to the generic kernel (bp.hip).
 hipError_t launch_bp_static(const DevCode &c, const BpLaunch &a, hipStream_t s);
 hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s);
+// Cooperative kernel for regular codes whose slots exceed the LDS: groups of
+// workgroups on one XCD share a codeword.  0 groups = not applicable.
+int bp_coop_groups(const DevCode &c);
+size_t bp_coop_sync_bytes(int groups);
+hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s);
+bool bp_coop_aborted(const BpLaunch &a, int groups, hipStream_t s);
 // Threads per workgroup of the regular kernel for this code shape, 0 if it does
 // not apply (host-side; decides whether upload_code builds the LDS plan).
 int bp_regular_threads(int N, int M, int E, int dv_max, int dc_max, int regular);
