@@ -333,6 +333,10 @@ hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const c
     hipError_t e = launch_bp_regular(c, a, s);
     if (e != hipErrorNotSupported) return e;
   }
+  if (lds && variant == 0) {
+    hipError_t e = launch_bp_irregular(c, a, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   if (lds && variant != 1) {
     hipError_t e = launch_bp_static(c, a, s);
     if (e != hipErrorNotSupported) return e;

@@ -191,6 +191,15 @@ int upload_code(kml_ctx *c) {
   d.is5g = L.is5g ? 1 : 0;
   d.active = L.active ? 1 : 0;
   d.regular = regular;
+  d.irr_ok = 1;
+  for (int j = 0; j < L.N; j++) {
+    const int dv = L.col_ptr[j + 1] - L.col_ptr[j];
+    if (dv < 1 || dv > 9) d.irr_ok = 0;
+  }
+  for (int i = 0; i < L.M; i++) {
+    const int dc = L.row_ptr[i + 1] - L.row_ptr[i];
+    if (dc < 2 || dc > 10) d.irr_ok = 0;
+  }
 
   HIPCHK(c, c->d_cons.ensure(sizeof(double) * (c->modem.pts.size() + 8)), "hipMalloc(cons)");
   kml::rotation_factors(c->rot);

@@ -22,6 +22,7 @@ struct DevCode {
   const uint64_t *enc_info;
   int M, N, E, K, cc_len, punct, info_off, chk, Kw, dv_max, dc_max, is5g, active;
   int regular;  // every column has degree dv_max and every row dc_max
+  int irr_ok;   // column degrees in [1, 9] and row degrees in [2, 10] (bp_irregular.hip)
   // LDS placement plan of bp_regular.hip (layout.hpp); null when the code does
   // not take that kernel.  vn_order then holds the planned column order.
   const int32_t *reg_c2v;  // aligned with col_slot: byte offset of the c2v message
@@ -73,6 +74,7 @@ struct BpLaunch {
 // fits it, else to the generic kernel (bp.hip).
 hipError_t launch_bp_static(const DevCode &c, const BpLaunch &a, hipStream_t s);
 hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s);
+hipError_t launch_bp_irregular(const DevCode &c, const BpLaunch &a, hipStream_t s);
 // Cooperative kernel for regular codes whose slots exceed the LDS: groups of
 // workgroups on one XCD share a codeword.  0 groups = not applicable.
 int bp_coop_groups(const DevCode &c);
