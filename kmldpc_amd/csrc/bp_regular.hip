@@ -120,12 +120,13 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
       for (int k = 0; k < H; ++k) p ^= cch[ccol[r][k]];
       fail |= p ^ swap_pair_i(p);
     }
-    if (!__syncthreads_or(fail)) {
-      conv = true;
-      break;
-    }
+    // The OR over the workgroup is folded into the CN phase's closing barrier:
+    // the CN phase runs speculatively, and a converged codeword (no failing
+    // row) discards it — its slots are never read again and its syndromes are
+    // only written when the phase counts.
 
     // ------------------------------------------------------------ CN phase
+    double syn0[RC];
     // Step s of the even lane advances alpha over edge s, of the odd lane beta
     // over edge DC-1-s.  From step H on, the pair swaps the chain states and
     // each lane finishes one c2v per step.  Within a step every message LOAD is
@@ -179,13 +180,18 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
           }
         }
       }
-      if constexpr (SYN) {
 #pragma unroll
-        for (int r = 0; r < RC; ++r)
-          if (!odd) a.syn[(long long)cw * c.M + crow[r]] = s0[r];  // alpha past the last edge (:274)
-      }
+      for (int r = 0; r < RC; ++r) syn0[r] = s0[r];
     }
-    __syncthreads();
+    if (!__syncthreads_or(fail)) {  // every row satisfied before this CN phase
+      conv = true;
+      break;
+    }
+    if constexpr (SYN) {
+#pragma unroll
+      for (int r = 0; r < RC; ++r)
+        if (!odd) a.syn[(long long)cw * c.M + crow[r]] = syn0[r];  // alpha past the last edge (:274)
+    }
   }
   iter_out = iter;
   conv_out = conv;
