@@ -188,22 +188,31 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
       const int full = p ^ swap_pair_i(p);
       if (d > 0) fail |= full;
     }
+    // the OR over the workgroup is folded into the CN phase's closing barrier
+    // (speculative CN, as in bp_regular.hip); syndromes are kept until the
+    // phase is known to count
+    double sv[RC];
+#pragma unroll
+    for (int r = 0; r < RC; ++r) {
+      const int q = (r * T + tid) >> 1;
+      sv[r] = 0.0;
+      if (q < c.M) {  // both lanes of a pair agree
+        const int row = c.cn_order[q];
+        const int base = c.row_ptr[row];
+        sv[r] = cn_any<SYN, FAST>(c.row_ptr[row + 1] - base, slots, base, odd);
+      }
+    }
     if (!__syncthreads_or(fail)) {
       conv = true;
       break;
     }
-
-#pragma unroll 1
-    for (int r = 0; r < RC; ++r) {
-      const int q = (r * T + tid) >> 1;
-      if (q < c.M) {  // both lanes of a pair agree
-        const int row = c.cn_order[q];
-        const int base = c.row_ptr[row];
-        const double sv = cn_any<SYN, FAST>(c.row_ptr[row + 1] - base, slots, base, odd);
-        if (SYN && !odd) a.syn[(long long)cw * c.M + row] = sv;  // alpha past the last edge (:274)
+    if constexpr (SYN) {
+#pragma unroll
+      for (int r = 0; r < RC; ++r) {
+        const int q = (r * T + tid) >> 1;
+        if (q < c.M && !odd) a.syn[(long long)cw * c.M + c.cn_order[q]] = sv[r];  // alpha past the last edge (:274)
       }
     }
-    __syncthreads();
   }
   iter_out = iter;
   conv_out = conv;
