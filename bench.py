@@ -122,23 +122,31 @@ def main():
     ap.add_argument("--seed", type=int, default=17)
     ap.add_argument("--cpu-cw-per-thread", type=int, default=5000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (RCCL over xGMI, the production path) or gloo (CPU counters; lets N ranks share "
+                         "fewer GPUs for testing)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = local
     if world > 1:
         import torch
         import torch.distributed as dist_mod
 
-        torch.cuda.set_device(local)
-        dist_mod.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist_mod.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:  # gloo: counters reduced on the CPU; ranks may share a GPU (tests on a 1-GPU box)
+            device = local % max(torch.cuda.device_count(), 1)
+            dist_mod.init_process_group(backend="gloo")
         dist = dist_mod
 
     d = data_dir()
     cfg = write_config(d, args)
-    ctx = K.Context(cfg, data_dir=d, device=local)
+    ctx = K.Context(cfg, data_dir=d, device=device)
     B = args.batch
     # frames for global codeword indices [rank*B, (rank+1)*B): resident in HBM
     ctx.sim_generate(args.snr, B, seed=args.seed, first_cw=rank * B)
@@ -146,8 +154,9 @@ def main():
     def barrier():
         ctx.sync()
         if dist is not None:
-            import torch
-            torch.cuda.synchronize()
+            if args.dist_backend == "nccl":
+                import torch
+                torch.cuda.synchronize()
             dist.barrier()
 
     for _ in range(args.warmup):
@@ -173,10 +182,11 @@ def main():
     t_max = elapsed
     if dist is not None:
         import torch
-        tv = torch.tensor(vals, device="cuda")
+        dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+        tv = torch.tensor(vals, device=dev)
         dist.all_reduce(tv)  # RCCL over xGMI: the only collective
         vals = tv.cpu().numpy()
-        tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
 
