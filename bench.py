@@ -203,12 +203,22 @@ def main():
     achieved_gbs = bp_bytes / (bp_avg_ms * 1e-3) / 1e9 if bp_avg_ms > 0 else 0.0
     achieved_tf = bp_flops / (bp_avg_ms * 1e-3) / 1e12 if bp_avg_ms > 0 else 0.0
     traffic = None
+    issue_view = None
     pmc = os.path.join(REPO, "profiles", "pmc_bp.json")
     if os.path.exists(pmc):
         try:
             pm = json.load(open(pmc))
-            if pm.get("batch") == B and pm.get("workload") == args.matrix:
+            if pm.get("batch") == B and pm.get("workload") == args.matrix and not args.blind:
                 traffic = pm.get("hbm_bytes_per_launch")
+                if pm.get("valu_issue_busy_frac") is not None:
+                    issue_view = {
+                        "valu_issue_busy_frac": pm["valu_issue_busy_frac"],
+                        "valu_wave_instr_per_launch": pm["valu_wave_instr_per_launch"],
+                        "rule": "PMC (profiles/pmc_bp.json): SIMD cycles the VALU instruction stream occupies "
+                                "(4 per wave64 instruction, 16 per v_rcp_f64) / SIMD cycles of the launch; the fp64 "
+                                "peak above assumes every instruction is an FMA, this kernel's exact-division "
+                                "arithmetic is 52% FMA, 28% MUL, 13% ADD, 7% rcp",
+                    }
         except Exception:
             traffic = None
     line = {
@@ -246,6 +256,7 @@ def main():
             "alg_flops_per_launch": round(bp_flops),
             "alg_flops_rule": "per executed VN phase sum_cols (68*d-23), per CN phase sum_rows (73*d-52) fp64 flops "
                               "(DESIGN.md: Roofline)",
+            "issue_view": issue_view,
             "hbm_view": {
                 "alg_bytes_per_launch": round(bp_bytes),
                 "achieved_GBs": round(achieved_gbs, 1),

@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--batch", type=int)
     ap.add_argument("--workload")
     ap.add_argument("--alg-bytes-per-launch", type=float)
+    ap.add_argument("--waves-per-simd", type=float, help="resident waves per SIMD of the kernel (issue view)")
     args = ap.parse_args()
     rows = []
     for d in args.dirs:
@@ -67,6 +68,20 @@ def main():
             out["hbm_bytes_per_launch_uncorrected"] = (fetch + write) * 1024
         if args.alg_bytes_per_launch:
             out["alg_bytes_per_launch"] = args.alg_bytes_per_launch
+        # VALU issue view: every wave64 VALU instruction holds a SIMD for 4
+        # cycles, v_rcp_f64 (TRANS) for 16; the wave's lifetime in cycles is
+        # 4 x SQ_WAVE_CYCLES (quad-cycles); waves per CU = 4 per SIMD here.
+        valu = res.get("SQ_INSTS_VALU", (None, 0))[0]
+        trans = res.get("SQ_INSTS_VALU_TRANS_F64", (None, 0))[0]
+        wave_q = res.get("SQ_WAVE_CYCLES", (None, 0))[0]
+        if valu and trans is not None and wave_q and args.waves_per_simd:
+            issue = (valu - trans) * 4 + trans * 16
+            simd_cycles = wave_q * 4 / args.waves_per_simd  # waves share a SIMD
+            out["valu_wave_instr_per_launch"] = valu
+            out["trans_f64_per_launch"] = trans
+            out["valu_issue_cycles_per_launch"] = issue
+            out["simd_cycles_per_launch"] = simd_cycles
+            out["valu_issue_busy_frac"] = round(issue / simd_cycles, 4)
         with open(args.json, "w") as f:
             json.dump(out, f, indent=1)
         print(json.dumps(out))
