@@ -325,37 +325,47 @@ def test_blind_gpu_monte_carlo(data_dir):
     assert abs(fer - ref) < 4 * sigma
 
 
-def test_empty_and_ragged_batches(data_dir):
-    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+CODES = [("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, 20),   # bp_regular_kernel (LDS)
+         ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, 50),  # bp_irregular_kernel (LDS)
+         ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 20)]  # bp_coop_kernel (L2 slots)
+
+
+@pytest.mark.parametrize("matrix,modem,is5g,max_iter", CODES)
+def test_empty_and_ragged_batches(data_dir, matrix, modem, is5g, max_iter):
+    ctx = ctx_for(data_dir, matrix, modem, is5g, max_iter)
     r = ctx.bp_decode(np.zeros((0, ctx.cc_len)))
     assert r["uu_hat"].shape == (0, ctx.K)
     # odd batch sizes around the grid size
     rng = np.random.default_rng(9)
+    oc = oracle_for(data_dir, matrix, is5g, max_iter)
     for B in (1, 3, 257, 513):
         p0 = rng.uniform(0.05, 0.95, (B, ctx.cc_len))
         r = ctx.bp_decode(p0, iter_count=3)
-        oc = oracle_for(data_dir, "PEG2304regular0.5.txt", False)
         for i in (0, B - 1):
             ret, uh, _, _ = oc.bp_decode(p0[i], 3)
             assert r["ret"][i] == ret and np.array_equal(r["uu_hat"][i], uh)
 
 
-def test_extreme_inputs_match_oracle(data_dir):
+@pytest.mark.parametrize("matrix,modem,is5g,max_iter", CODES)
+def test_extreme_inputs_match_oracle(data_dir, matrix, modem, is5g, max_iter):
     """Saturated / tie / NaN-free edge inputs: P0 at the clip bounds, exactly
-    0.5 everywhere (every hard decision is a tie -> 1), and 0/1 extremes."""
-    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
-    oc = oracle_for(data_dir, "PEG2304regular0.5.txt", False)
+    0.5 everywhere (every hard decision is a tie -> 1), 0/1 extremes, and -0.0
+    and subnormal priors (outside the fast-division domain: the IEEE path)."""
+    ctx = ctx_for(data_dir, matrix, modem, is5g, max_iter)
+    oc = oracle_for(data_dir, matrix, is5g, max_iter)
     n = ctx.cc_len
     rng = np.random.default_rng(4)
     cases = [np.full(n, 0.5), np.full(n, 1e-12), np.full(n, 1 - 1e-12),
-             np.where(rng.random(n) < 0.5, 1e-12, 1 - 1e-12), rng.choice([0.0, 1.0, 0.5], n)]
+             np.where(rng.random(n) < 0.5, 1e-12, 1 - 1e-12), rng.choice([0.0, 1.0, 0.5], n),
+             np.where(rng.random(n) < 0.3, -0.0, rng.uniform(0.2, 0.8, n)),
+             np.where(rng.random(n) < 0.3, 5e-320, rng.uniform(0.2, 0.8, n))]
     p0 = np.stack(cases)
     r = ctx.bp_decode(p0, cc_hat=True, syn=np.zeros((len(cases), ctx.M)))
     for i in range(len(cases)):
         ret, uh, cch, syn = oc.bp_decode(p0[i])
-        assert r["ret"][i] == ret
-        assert np.array_equal(r["cc_hat"][i], cch)
-        assert np.array_equal(r["syn"][i], syn, equal_nan=True)
+        assert r["ret"][i] == ret, i
+        assert np.array_equal(r["cc_hat"][i], cch), i
+        assert np.array_equal(r["syn"][i], syn, equal_nan=True), i
 
 
 # ---------------------------------------------------------------- soft metric
