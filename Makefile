@@ -9,7 +9,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall 
 CSRC     := kmldpc_amd/csrc
 OBJDIR   := build/obj
 CPP_SRCS := config code modem layout capi simulate refstream
-HIP_SRCS := bp bp_static bp_regular bp_irregular bp_coop demap kmeans framegen
+HIP_SRCS := bp bp_regular bp_irregular bp_coop demap kmeans framegen
 OBJS     := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(CPP_SRCS) $(HIP_SRCS)))
 HDRS     := $(wildcard $(CSRC)/*.hpp) include/kmldpc_amd.h
 LIB      := kmldpc_amd/libkmldpc_amd.so

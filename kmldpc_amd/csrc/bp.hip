@@ -293,14 +293,12 @@ hipError_t dispatch_deg(const DevCode &c, const BpLaunch &a, unsigned int *queue
 }  // namespace
 
 namespace {
-// KML_BP_KERNEL=generic|static forces a kernel family (A/B measurements).
+// KML_BP_KERNEL=generic forces the generic kernel (A/B measurements).
 int kernel_variant() {
   static int v = -1;
   if (v < 0) {
     const char *e = getenv("KML_BP_KERNEL");
-    v = 0;
-    if (e && e[0] == 'g') v = 1;
-    if (e && e[0] == 's') v = 2;
+    v = (e && e[0] == 'g') ? 1 : 0;
   }
   return v;
 }
@@ -328,17 +326,15 @@ hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const c
     return hipErrorInvalidValue;
   }
   const bool lds = bp_uses_lds(c);
-  const int variant = kernel_variant();  // 0 auto, 1 generic, 2 static
+  // kernel families, most specialised first: regular PEG2304-class (LDS),
+  // irregular with degrees <= 9 / 10 (LDS), cooperative regular (L2), generic
+  const int variant = kernel_variant();  // 0 auto, 1 generic
   if (lds && variant == 0) {
     hipError_t e = launch_bp_regular(c, a, s);
     if (e != hipErrorNotSupported) return e;
   }
   if (lds && variant == 0) {
     hipError_t e = launch_bp_irregular(c, a, s);
-    if (e != hipErrorNotSupported) return e;
-  }
-  if (lds && variant != 1) {
-    hipError_t e = launch_bp_static(c, a, s);
     if (e != hipErrorNotSupported) return e;
   }
   if (!lds && variant == 0) {

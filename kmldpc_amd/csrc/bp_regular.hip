@@ -2,7 +2,7 @@
 // message state fits in LDS (PEG2304: dv = 3, dc = 6, 6912 edges).
 //
 // Arithmetic: bit-exact restatement of lab::BinaryLDPCCodec::Decoder
-// (lib/lab/src/binaryldpccodec.cc:165-278), like bp.hip / bp_static.hip.
+// (lib/lab/src/binaryldpccodec.cc:165-278), like bp.hip.
 //
 // Mapping onto a gfx950 CU (one workgroup of T threads per CU, all message
 // slots in LDS, persistent over codewords via a dequeue counter):

@@ -69,10 +69,6 @@ struct BpLaunch {
   unsigned int *queue = nullptr; // 4-byte device dequeue counter (zeroed by the launcher)
 };
 
-// Returns hipSuccess or an error; `err` is set for configuration problems.
-// Dispatches to the static-assignment LDS kernel (bp_static.hip) when the code
-// fits it, else to the generic kernel (bp.hip).
-hipError_t launch_bp_static(const DevCode &c, const BpLaunch &a, hipStream_t s);
 hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s);
 hipError_t launch_bp_irregular(const DevCode &c, const BpLaunch &a, hipStream_t s);
 // Cooperative kernel for regular codes whose slots exceed the LDS: groups of
