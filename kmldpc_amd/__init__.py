@@ -25,7 +25,7 @@ import numpy as np
 __all__ = ["Context", "KmlError", "lib", "LIB_PATH", "BinaryLDPCCodec", "KMeans", "KmCodec"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkmldpc_amd.so")
+LIB_PATH = os.environ.get("KML_LIB") or os.path.join(HERE, "libkmldpc_amd.so")  # KML_LIB: A/B builds
 INCLUDE = os.path.join(os.path.dirname(HERE), "include", "kmldpc_amd.h")
 
 KML_DEVICE_PTRS = 1
