@@ -30,6 +30,12 @@ import kmldpc_amd as K  # noqa: E402
 
 K.lib()  # load the HIP library (and its ROCm runtime) before torch
 
+KERNEL_NOTES = {
+    "bp_regular_kernel": "sum-product BP, messages LDS-resident",
+    "bp_irregular_kernel": "sum-product BP, irregular degrees, messages LDS-resident",
+    "bp_coop_kernel": "sum-product BP, 4 workgroups per codeword, messages in L2",
+    "bp_kernel": "sum-product BP, generic",
+}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 dense peak (vector = matrix rate, AMD spec)
 
@@ -172,6 +178,7 @@ def main():
     ctx.prof_enable(False)
     elapsed = t1 - t0
     bp = ctx.prof_read("bp")
+    bp_kernel = ctx.bp_kernel()
     stages = {s: ctx.prof_read(s) for s in ("demap", "kmeans", "metric")}
     # one more (untimed) pass for the statistical counters
     c = ctx.sim_decode(args.snr, blind=args.blind)
@@ -208,7 +215,8 @@ def main():
     if os.path.exists(pmc):
         try:
             pm = json.load(open(pmc))
-            if pm.get("batch") == B and pm.get("workload") == args.matrix and not args.blind:
+            if (pm.get("batch") == B and pm.get("workload") == args.matrix and not args.blind
+                    and pm.get("kernel") == bp_kernel):
                 traffic = pm.get("hbm_bytes_per_launch")
                 if pm.get("valu_issue_busy_frac") is not None:
                     issue_view = {
@@ -251,7 +259,7 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 4),
             "traffic": traffic,
-            "kernel": "bp_regular_kernel (sum-product BP, messages LDS-resident)",
+            "kernel": f"{bp_kernel} ({KERNEL_NOTES.get(bp_kernel, 'sum-product BP')})",
             "avg_launch_ms": round(bp_avg_ms, 4),
             "alg_flops_per_launch": round(bp_flops),
             "alg_flops_rule": "per executed VN phase sum_cols (68*d-23), per CN phase sum_rows (73*d-52) fp64 flops "

@@ -93,6 +93,9 @@ int kml_create_explicit(const char *matrix_file, const char *modem_file, int is5
 void kml_destroy(kml_ctx *ctx);
 const char *kml_last_error(const kml_ctx *ctx);
 int kml_abi_version(void);
+/* Name of the BP kernel family the context last launched ("bp_regular_kernel",
+ * "bp_irregular_kernel", "bp_coop_kernel", "bp_kernel"; "" before any decode). */
+const char *kml_bp_kernel(const kml_ctx *ctx);
 
 int kml_dims(const kml_ctx *ctx, int32_t *dims /* [KML_DIM_COUNT] */);
 /* Host-side code plan, for inspection and parity tests. */

@@ -66,6 +66,7 @@ def lib():
     PP = C.POINTER(C.c_void_p)
     sig = {
         "kml_abi_version": (I, []),
+        "kml_bp_kernel": (C.c_char_p, [P]),
         "kml_create": (I, [C.c_char_p, C.c_char_p, I, PP]),
         "kml_create_explicit": (I, [C.c_char_p, C.c_char_p, I, I, I, I, I, I, PP]),
         "kml_destroy": (None, [P]),
@@ -274,6 +275,10 @@ class Context:
         self._chk(lib().kml_sim_decode(self._h, float(snr), int(blind), _p(cnt), 1), "kml_sim_decode")
         return dict(zip(["err_bit", "err_blk", "tot_bit", "tot_blk", "vn_phases", "cn_phases", "converged"],
                         [int(x) for x in cnt[:7]]))
+
+    def bp_kernel(self):
+        """Name of the BP kernel family the last decode launched."""
+        return lib().kml_bp_kernel(self._h).decode()
 
     def sync(self):
         self._chk(lib().kml_sync(self._h), "kml_sync")

@@ -314,7 +314,7 @@ long long bp_gslots_needed(const DevCode &c) {
   return (long long)ncu * 4 * c.E;  // up to 4 resident workgroups per CU
 }
 
-hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const char **err) {
+hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const char **err, const char **family) {
   if (a.B <= 0) return hipSuccess;
   if (a.iter_count < 0) {
     if (err) *err = "iter_count must be >= 0";
@@ -331,21 +331,31 @@ hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const c
   const int variant = kernel_variant();  // 0 auto, 1 generic
   if (lds && variant == 0) {
     hipError_t e = launch_bp_regular(c, a, s);
-    if (e != hipErrorNotSupported) return e;
+    if (e != hipErrorNotSupported) {
+      if (family) *family = "bp_regular_kernel";
+      return e;
+    }
   }
   if (lds && variant == 0) {
     hipError_t e = launch_bp_irregular(c, a, s);
-    if (e != hipErrorNotSupported) return e;
+    if (e != hipErrorNotSupported) {
+      if (family) *family = "bp_irregular_kernel";
+      return e;
+    }
   }
   if (!lds && variant == 0) {
     hipError_t e = launch_bp_coop(c, a, s);
-    if (e != hipErrorNotSupported) return e;
+    if (e != hipErrorNotSupported) {
+      if (family) *family = "bp_coop_kernel";
+      return e;
+    }
   }
   if (!lds && (a.gslots == nullptr || a.gslots_cap < c.E)) {
     if (err) *err = "global slot workspace missing";
     return hipErrorInvalidValue;
   }
   const bool syn = a.syn != nullptr;
+  if (family) *family = "bp_kernel";
   if (lds) return syn ? dispatch_deg<true, true>(c, a, queue, s, err) : dispatch_deg<true, false>(c, a, queue, s, err);
   return syn ? dispatch_deg<false, true>(c, a, queue, s, err) : dispatch_deg<false, false>(c, a, queue, s, err);
 }

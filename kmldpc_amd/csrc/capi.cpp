@@ -66,6 +66,7 @@ constexpr int kArenaSlots = 1024;
 
 struct kml_ctx {
   int device = 0;
+  const char *bp_family = nullptr;  // kernel family of the last BP launch
   hipStream_t stream = nullptr;
   kml::RunConfig rc;
   kml::LdpcCode code;
@@ -325,7 +326,7 @@ int run_bp(kml_ctx *c, kml::BpLaunch a, int &slot_out, int reuse = -1) {
   if (c->coop_groups > 0) c->coop_pending = true;
   Timer t(c, "bp", slot, (double)a.B * 8.0 * c->code.cc_len);
   const char *msg = nullptr;
-  hipError_t e = kml::launch_bp(c->dc, a, c->stream, &msg);
+  hipError_t e = kml::launch_bp(c->dc, a, c->stream, &msg, &c->bp_family);
   t.stop();
   if (e != hipSuccess) return msg ? fail(c, KML_E_UNSUP, msg) : hip_fail(c, e, "bp launch");
   slot_out = slot;
@@ -790,6 +791,8 @@ void kml_destroy(kml_ctx *c) {
 }
 
 const char *kml_last_error(const kml_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+const char *kml_bp_kernel(const kml_ctx *c) { return c && c->bp_family ? c->bp_family : ""; }
 
 int kml_dims(const kml_ctx *c, int32_t *d) {
   if (!c || !d) return KML_E_ARG;

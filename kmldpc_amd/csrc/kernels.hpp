@@ -80,7 +80,9 @@ bool bp_coop_aborted(const BpLaunch &a, int groups, hipStream_t s);
 // Threads per workgroup of the regular kernel for this code shape, 0 if it does
 // not apply (host-side; decides whether upload_code builds the LDS plan).
 int bp_regular_threads(int N, int M, int E, int dv_max, int dc_max, int regular);
-hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const char **err);
+// family (optional) receives the name of the kernel that was launched.
+hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const char **err,
+                     const char **family = nullptr);
 // Workspace the BP launcher needs in global-slot mode (double2 elements).
 long long bp_gslots_needed(const DevCode &c);
 bool bp_uses_lds(const DevCode &c);
