@@ -132,6 +132,8 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
   bool conv = false;
   for (; iter < a.iter_count; ++iter) {
     // ------------------------------------------------------------ VN phase
+    // falling wave priorities within a phase (see bp_regular.hip)
+    __builtin_amdgcn_s_setprio(3);
     {
       double c0s[RV][DV];
 #pragma unroll
@@ -163,8 +165,11 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
       double b0[RV], b1[RV];
 #pragma unroll
       for (int r = 0; r < RV; ++r) b0[r] = b1[r] = 1.0;
+      __builtin_amdgcn_s_setprio(2);
 #pragma unroll
-      for (int k = DV - 1; k >= 0; --k)
+      for (int k = DV - 1; k >= 0; --k) {
+        if (k == DV - 2) __builtin_amdgcn_s_setprio(1);
+        if (k == DV - 3) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
         for (int r = 0; r < RV; ++r) {
           const bool unit = FAST && k == DV - 1;
@@ -180,6 +185,7 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
             div2<FAST>(n0, n1, n0 + n1, b0[r], b1[r]);
           }
         }
+      }
     }
     if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return false;
 
@@ -214,8 +220,11 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
         s0[r] = 1.0;
         s1[r] = 0.0;
       }
+      __builtin_amdgcn_s_setprio(2);
 #pragma unroll
       for (int st = 0; st < DC; ++st) {
+        if (st == 2) __builtin_amdgcn_s_setprio(1);
+        if (st == 4) __builtin_amdgcn_s_setprio(0);
         const bool advance = SYN || st + 1 < DC;
         double m0[RC], m1[RC];
         if (advance) {

@@ -121,6 +121,16 @@ __device__ __forceinline__ double cn_half(double2 *slots, int base, int odd) {
   return s0;
 }
 
+// falling wave priorities over a phase's rounds (see bp_regular.hip)
+__device__ __forceinline__ void set_prio(int p) {
+  switch (p) {
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    default: __builtin_amdgcn_s_setprio(0); break;
+  }
+}
+
 template <bool FAST>
 __device__ __forceinline__ void vn_any(int d, double2 *slots, const unsigned short *cs, double p, unsigned char *h) {
   switch (d) {
@@ -163,6 +173,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
     // the LDS priors, so nothing is indexed by round in registers
 #pragma unroll 1
     for (int r = 0; r < RV; ++r) {
+      set_prio(3 - r);
       const int pos = r * T + tid;
       if (pos < c.N) {
         const int v = c.vn_order[pos];
@@ -194,6 +205,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
     double sv[RC];
 #pragma unroll
     for (int r = 0; r < RC; ++r) {
+      set_prio(2 - r);
       const int q = (r * T + tid) >> 1;
       sv[r] = 0.0;
       if (q < c.M) {  // both lanes of a pair agree
