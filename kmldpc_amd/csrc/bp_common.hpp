@@ -57,6 +57,15 @@ __device__ __forceinline__ double div1(double n0, double s) {
   }
 }
 
+// The first backward step of a column multiplies beta = (1, 1) by the c2v pair
+// (c0, RN(1 - c0)) and normalises by s = RN(c0 + RN(1 - c0)).  For c0 in [0, 1]
+// s is exactly 1: for c0 >= 1/2, 1 - c0 is exact (Sterbenz); for c0 < 1/2 the
+// rounding error of 1 - c0 (in (1/2, 1]) is at most 2^-54, so the exact sum lies
+// in [1 - 2^-54, 1 + 2^-54], which rounds to 1 (1 - 2^-54 is a tie, broken to
+// the even 1).  Division by 1 is exact, so the FAST kernels take beta =
+// (c0, RN(1 - c0)) directly; c2v messages are always clipped to
+// [1e-12, 1 - 1e-12] or 0.5 on the FAST path.
+
 // Prior values for which the FAST division path is exact (see div2).
 // -0.0 is excluded: with every prior >= +0 no message is ever -0, which makes
 // the x*1.0 / (1,0)-state identities used on the FAST path exact.

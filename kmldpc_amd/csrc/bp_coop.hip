@@ -180,9 +180,12 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
           if (vact[r]) slots[es[r][k]] = make_double2(q0, q1);
           if (k > 0) {
             const double c0 = c0s[r][k];
-            const double n0 = unit ? c0 : b0[r] * c0;
-            const double n1 = unit ? (1.0 - c0) : b1[r] * (1.0 - c0);
-            div2<FAST>(n0, n1, n0 + n1, b0[r], b1[r]);
+            if (unit) {  // (c0, 1 - c0) / (c0 + (1 - c0)): the sum rounds to exactly 1 (bp_common.hpp)
+              b0[r] = c0;
+              b1[r] = 1.0 - c0;
+            } else {
+              div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r]);
+            }
           }
         }
       }

@@ -67,9 +67,12 @@ __device__ __forceinline__ void vn_column(double2 *slots, const unsigned short *
     slots[cs[k]] = make_double2(q0, q1);
     if (k > 0) {
       const double c0 = c0s[k];
-      const double n0 = unit ? c0 : b0 * c0;
-      const double n1 = unit ? (1.0 - c0) : b1 * (1.0 - c0);
-      div2<FAST>(n0, n1, n0 + n1, b0, b1);
+      if (unit) {  // (c0, 1 - c0) / (c0 + (1 - c0)): the sum rounds to exactly 1 (bp_common.hpp)
+        b0 = c0;
+        b1 = 1.0 - c0;
+      } else {
+        div2<FAST>(b0 * c0, b1 * (1.0 - c0), b0 * c0 + b1 * (1.0 - c0), b0, b1);
+      }
     }
   }
 }

@@ -218,3 +218,20 @@ def test_ref_frames_reproduce_reference_stream(case, data_dir):
         assert zlib.crc32(y[i].tobytes()) & 0xFFFFFFFF == z["s_crc_y"][i]
         assert zlib.crc32(uu[i].tobytes()) & 0xFFFFFFFF == z["s_crc_uu"][i]
     assert np.array_equal(th, z["s_true_h"][:n])
+
+
+def test_first_backward_normalisation_is_identity():
+    """bp_common.hpp: RN(c0 + RN(1 - c0)) == 1 for every c0 in [0, 1], so the
+    FAST kernels skip the first backward normalisation of each column."""
+    rng = np.random.default_rng(5)
+    c0 = np.concatenate([
+        rng.random(2_000_000),
+        rng.random(500_000) * 1e-6,  # small messages, where 1 - c0 rounds
+        1.0 - rng.random(500_000) * 1e-6,
+        np.ldexp(rng.random(500_000) + 0.5, rng.integers(-40, 0, 500_000)),
+        np.array([0.0, 1.0, 0.5, 1e-12, 1.0 - 1e-12, np.nextafter(0.5, 0.0), np.nextafter(0.5, 1.0),
+                  np.nextafter(1.0, 0.0), 5e-324]),
+    ])
+    one_minus = 1.0 - c0
+    assert np.all(c0 + one_minus == 1.0)
+    assert np.all(c0 / (c0 + one_minus) == c0) and np.all(one_minus / (c0 + one_minus) == one_minus)
