@@ -328,6 +328,17 @@ def test_blind_gpu_monte_carlo(data_dir):
 CODES = [("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, 20),   # bp_regular_kernel (LDS)
          ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, 50),  # bp_irregular_kernel (LDS)
          ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 20)]  # bp_coop_kernel (L2 slots)
+FAMILY = {"PEG2304regular0.5.txt": "bp_regular_kernel", "5GLDPCBG2a3_R12_K960.txt": "bp_irregular_kernel",
+          "PEG8064regular0.5.txt": "bp_coop_kernel"}
+
+
+@pytest.mark.parametrize("matrix,modem,is5g,max_iter", CODES)
+def test_dispatch_takes_the_specialised_kernel(data_dir, matrix, modem, is5g, max_iter):
+    """Each code runs on its own kernel family (so the parity tests below cover
+    all three), not on the generic fallback."""
+    ctx = ctx_for(data_dir, matrix, modem, is5g, max_iter)
+    ctx.bp_decode(np.full((2, ctx.cc_len), 0.3), iter_count=2)
+    assert ctx.bp_kernel() == FAMILY[matrix]
 
 
 @pytest.mark.parametrize("matrix,modem,is5g,max_iter", CODES)
