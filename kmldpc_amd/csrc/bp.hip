@@ -346,7 +346,7 @@ hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const c
   if (!lds && variant == 0) {
     hipError_t e = launch_bp_coop(c, a, s);
     if (e != hipErrorNotSupported) {
-      if (family) *family = "bp_coop_kernel";
+      if (family) *family = bp_coop_family(c);
       return e;
     }
   }

@@ -34,6 +34,8 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include <algorithm>
+
 #include "bp_common.hpp"
 #include "kernels.hpp"
 
@@ -51,6 +53,14 @@ struct GroupSync {
   unsigned pcnt;     // unsatisfied checks of the final hard decisions, summed
   unsigned xcc;      // bit per XCD a member runs on
 };
+
+constexpr int kPartG = 4;  // workgroups per codeword of the partitioned kernel
+
+// LDS of the partitioned kernel: the member's row slots, its mirror slots, and
+// every column's hard decision.
+size_t part_lds_bytes(const DevCode &c) {
+  return ((size_t)c.M / kPartG * 6 + (size_t)c.pt_mirror) * 16 + (size_t)c.N;
+}
 
 constexpr long long kSpinLimit = 20000000;  // ~1 s of s_sleep(1) polls
 
@@ -444,6 +454,407 @@ __global__ __launch_bounds__(T) void bp_coop_kernel(DevCode c, BpLaunch a, Group
   }
 }
 
+// ===========================================================================
+// Partitioned cooperative kernel (bp_part_kernel): the group mapping and the
+// group barriers above, but every message access of the arithmetic is an LDS
+// access.  Member m keeps the 16-byte slots of ITS rows in LDS, plus one
+// MIRROR slot per cut edge of its columns (an edge whose row another member
+// owns; layout.hpp PartitionPlan).  The planner's partition cuts ~27% of
+// PEG8064's edges; those messages cross members through two mailboxes in the
+// group's global scratch, copied by short coalesced loops around the group
+// barriers:
+//   VN compute (row slots + mirrors) -> send v2c (mirrors -> v2c mailbox)
+//   -> barrier -> receive v2c (mailbox -> row slots) and the other members'
+//   hard decisions -> parity check + CN compute (row slots) -> send c2v (row
+//   slots -> c2v mailbox) -> barrier -> receive c2v (mailbox -> mirrors).
+// The global-slot kernel above gathers and scatters every edge's message
+// through the XCD's L2 at 8-16 bytes per lane, which bounds its iterations
+// by the L2 request rate; here the exchange moves ~24 bytes per cut edge per
+// iteration in mostly contiguous runs.
+
+template <int kG, int RV, int RC, int RX, bool SYN, bool FAST>
+__device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N, int NG, int cw, GroupSync *gs,
+                                                unsigned &gen, bool same_xcd, unsigned *abort, unsigned char *smem,
+                                                uint8_t *dec, double2 *mb_v2c, double *mb_c2v, uint8_t *gc,
+                                                const int (&vaddr)[RV][3], const int (&vpos)[RV],
+                                                const bool (&vact)[RV], const double (&pv)[RV], const int (&crow)[RC],
+                                                const int (&cbase)[RC], const int (&ccol)[RC][3],
+                                                const bool (&cact)[RC], const int (&xr)[RX], const int (&xc)[RX],
+                                                int odd, int member, int &iter_out, bool &conv_out) {
+  constexpr int DV = 3, DC = 6, H = 3;
+  const int tid = threadIdx.x;
+  double2 *slots = reinterpret_cast<double2 *>(smem);
+  int iter = 0;
+  bool conv = false;
+  for (; iter < a.iter_count; ++iter) {
+    // ---------------------------------- receive c2v of the cut edges (mirrors)
+    if (iter > 0) {  // iteration 0 reads InitMsg's 0.5
+#pragma unroll
+      for (int q = 0; q < RX; ++q)
+        if (xc[q] >= 0) *reinterpret_cast<double *>(smem + (xc[q] & 0xFFFF) * 16) = ld_nt(&mb_c2v[xc[q] >> 16]);
+      __syncthreads();
+    }
+    // ------------------------------------------------------------ VN phase
+    __builtin_amdgcn_s_setprio(3);
+    {
+      double c0s[RV][DV];
+#pragma unroll
+      for (int r = 0; r < RV; ++r)
+#pragma unroll
+        for (int k = 0; k < DV; ++k) c0s[r][k] = *reinterpret_cast<const double *>(smem + vaddr[r][k]);
+      double a0[RV], a1[RV], al0[RV][DV], al1[RV][DV];
+#pragma unroll
+      for (int r = 0; r < RV; ++r) {
+        a0[r] = pv[r];
+        a1[r] = 1.0 - pv[r];
+      }
+#pragma unroll
+      for (int k = 0; k < DV; ++k)
+#pragma unroll
+        for (int r = 0; r < RV; ++r) {
+          al0[r][k] = a0[r];
+          al1[r][k] = a1[r];
+          const double c0 = c0s[r][k];
+          const double n0 = a0[r] * c0;
+          const double n1 = a1[r] * (1.0 - c0);
+          if (k + 1 < DV) {
+            div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r]);
+          } else {
+            const int hd = hard_decision<FAST>(n0, n1);
+            if (vact[r]) {
+              dec[vpos[r]] = (unsigned char)hd;
+              gc[vpos[r]] = (unsigned char)hd;
+            }
+          }
+        }
+      double b0[RV], b1[RV];
+#pragma unroll
+      for (int r = 0; r < RV; ++r) b0[r] = b1[r] = 1.0;
+      __builtin_amdgcn_s_setprio(2);
+#pragma unroll
+      for (int k = DV - 1; k >= 0; --k) {
+        if (k == DV - 2) __builtin_amdgcn_s_setprio(1);
+        if (k == DV - 3) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+        for (int r = 0; r < RV; ++r) {
+          const bool unit = FAST && k == DV - 1;
+          const double t0 = unit ? al0[r][k] : al0[r][k] * b0[r];
+          const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
+          double q0, q1;
+          div2<FAST>(t0, t1, t0 + t1, q0, q1);
+          if (vact[r]) *reinterpret_cast<double2 *>(smem + vaddr[r][k]) = make_double2(q0, q1);
+          if (k > 0) {
+            const double c0 = c0s[r][k];
+            if (unit) {  // the sum rounds to exactly 1 (bp_common.hpp)
+              b0[r] = c0;
+              b1[r] = 1.0 - c0;
+            } else {
+              div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r]);
+            }
+          }
+        }
+      }
+    }
+    // ---------------------------------------------- send v2c of the cut edges
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < RX; ++q)
+      if (xc[q] >= 0) mb_v2c[xc[q] >> 16] = slots[xc[q] & 0xFFFF];
+    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return false;
+
+    // ------------------- receive v2c and the other members' hard decisions
+#pragma unroll
+    for (int q = 0; q < RX; ++q)
+      if (xr[q] >= 0) slots[xr[q] & 0xFFFF] = ld_nt(&mb_v2c[xr[q] >> 16]);
+    for (int i = tid; i < (kG - 1) * (NG / 16); i += blockDim.x) {
+      int m = i / (NG / 16);
+      const int off = (m + (m >= member)) * NG + (i - m * (NG / 16)) * 16;
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(gc + off));
+      *reinterpret_cast<u32x4 *>(dec + off) = v;
+    }
+    __syncthreads();
+
+    // -------------------- early-stop parity check, folded into the CN barrier
+    {
+      int fail = 0;
+#pragma unroll
+      for (int r = 0; r < RC; ++r) {
+        int p = 0;
+#pragma unroll
+        for (int k = 0; k < H; ++k) p ^= dec[ccol[r][k]];
+        fail |= cact[r] ? (p ^ swap_pair_i(p)) : 0;
+      }
+      if (__ballot(fail) != 0 && (tid & 63) == 0)
+        __hip_atomic_fetch_or(&gs->flag[iter & 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+    // ------------------------------------------------------------ CN phase
+    // (bp_regular.hip's step order: every load of a step before its stores)
+    double syn0[RC];
+    {
+      double x0[RC][H], x1[RC][H];
+      double s0[RC], s1[RC];
+#pragma unroll
+      for (int r = 0; r < RC; ++r) {
+        s0[r] = 1.0;
+        s1[r] = 0.0;
+      }
+      __builtin_amdgcn_s_setprio(2);
+#pragma unroll
+      for (int st = 0; st < DC; ++st) {
+        if (st == 2) __builtin_amdgcn_s_setprio(1);
+        if (st == 4) __builtin_amdgcn_s_setprio(0);
+        const bool advance = SYN || st + 1 < DC;
+        double m0[RC], m1[RC];
+        if (advance) {
+#pragma unroll
+          for (int r = 0; r < RC; ++r) {
+            const double2 m = *reinterpret_cast<const double2 *>(smem + cbase[r] + (odd ? DC - 1 - st : st) * 16);
+            m0[r] = m.x;
+            m1[r] = m.y;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < RC; ++r) {
+          if (st < H) {
+            x0[r][st] = s0[r];
+            x1[r][st] = s1[r];
+          } else {
+            const double y0 = swap_pair(s0[r]);
+            const double y1 = swap_pair(s1[r]);
+            const double o0 = x0[r][DC - 1 - st], o1 = x1[r][DC - 1 - st];
+            const bool unit = FAST && st == DC - 1;
+            const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
+            const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
+            const double q = clip_c2v<FAST>(div1<FAST>(t0, t0 + t1));
+            if (cact[r]) *reinterpret_cast<double *>(smem + cbase[r] + (odd ? st : DC - 1 - st) * 16) = q;
+          }
+        }
+        if (advance) {
+#pragma unroll
+          for (int r = 0; r < RC; ++r) {
+            const bool unit = FAST && st == 0;
+            const double n0 = unit ? m0[r] : s0[r] * m0[r] + s1[r] * m1[r];
+            const double n1 = unit ? m1[r] : s0[r] * m1[r] + s1[r] * m0[r];
+            div2<FAST>(n0, n1, n0 + n1, s0[r], s1[r]);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RC; ++r) syn0[r] = s0[r];
+    }
+    // ---------------------------------------------- send c2v of the cut edges
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < RX; ++q)
+      if (xr[q] >= 0) mb_c2v[xr[q] >> 16] = slots[xr[q] & 0xFFFF].x;
+    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return false;
+    if (!ld_rlx(&gs->flag[iter & 1])) {  // every row satisfied: stop before this CN phase
+      conv = true;
+      break;
+    }
+    if (member == 0 && tid == 0)  // cleared before anyone can OR into it (next VN barrier)
+      __hip_atomic_store(&gs->flag[(iter + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (SYN) {
+#pragma unroll
+      for (int r = 0; r < RC; ++r)
+        if (cact[r] && !odd) a.syn[(long long)cw * M + crow[r]] = syn0[r];  // alpha past the last edge (:274)
+    }
+  }
+  iter_out = iter;
+  conv_out = conv;
+  return true;
+}
+
+template <int kG, int T, int RV, int RC, int RX, bool SYN>
+__global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, GroupSync *gsync, uint8_t *gcch,
+                                                    unsigned *abort, unsigned int *queue, int fast_allowed) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int DV = 3, DC = 6, H = 3;
+  const int tid = threadIdx.x;
+  const int odd = tid & 1;
+  const int member = (blockIdx.x >> 3) % kG;
+  const int group = (blockIdx.x / (8 * kG)) * 8 + (blockIdx.x & 7);
+  GroupSync *gs = gsync + group;
+  const int MG = c.M / kG, NG = c.N / kG, EG = MG * DC;
+  double2 *mb_v2c = a.gslots + (size_t)group * c.E;       // [ncut] double2
+  double *mb_c2v = reinterpret_cast<double *>(mb_v2c + c.pt_ncut);  // [ncut] double
+  uint8_t *gc = gcch + (size_t)group * c.N;
+  const int nslots = EG + c.pt_mirror;
+  uint8_t *dec = smem + (size_t)nslots * 16;  // N hard decisions, plan order
+
+  int vaddr[RV][DV], vpos[RV];
+  bool vact[RV];
+#pragma unroll
+  for (int r = 0; r < RV; ++r) {
+    const int i = r * T + tid;
+    vact[r] = i < NG;
+    vpos[r] = member * NG + (vact[r] ? i : 0);
+#pragma unroll
+    for (int k = 0; k < DV; ++k) vaddr[r][k] = c.pt_vaddr[vpos[r] * DV + k];
+  }
+  int crow[RC], cbase[RC], ccol[RC][H];
+  bool cact[RC];
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int i = (r * T + tid) >> 1;  // lane pairs share a row
+    cact[r] = i < MG;
+    const int li = cact[r] ? i : 0;
+    const int row = c.pt_cn[member * MG + li];
+    crow[r] = row;
+    cbase[r] = li * DC * 16;
+#pragma unroll
+    for (int k = 0; k < H; ++k) ccol[r][k] = c.pt_pos[c.row_col[c.row_ptr[row] + (odd ? H + k : k)]];
+  }
+  int xr[RX], xc[RX];
+  {
+    const int r0 = c.pt_xr_ptr[member], r1 = c.pt_xr_ptr[member + 1];
+    const int c0 = c.pt_xc_ptr[member], c1 = c.pt_xc_ptr[member + 1];
+#pragma unroll
+    for (int q = 0; q < RX; ++q) {
+      const int i = q * T + tid;
+      xr[q] = r0 + i < r1 ? c.pt_xr[r0 + i] : -1;
+      xc[q] = c0 + i < c1 ? c.pt_xc[c0 + i] : -1;
+    }
+  }
+
+  unsigned gen = 0;
+  if (tid == 0) {
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
+    __hip_atomic_fetch_or(&gs->xcc, 1u << xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (!group_barrier<kG>(gs, gen, false, abort)) return;
+  const bool same_xcd = __popc(ld_rlx(&gs->xcc)) == 1;
+
+  for (;;) {
+    if (member == 0 && tid == 0) {
+      __hip_atomic_store(&gs->cw, atomicAdd(queue, 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&gs->nofast, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&gs->errs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&gs->pcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&gs->flag[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&gs->flag[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return;
+    const int entry = (int)ld_rlx(&gs->cw);
+    if (entry >= a.B) break;
+    const int cw = a.cw_idx ? a.cw_idx[entry] : entry;
+    const double *p0 = a.p0 + (long long)cw * a.p0_stride;
+    if (a.p0_sel) p0 += (long long)a.p0_sel[cw] * a.p0_sel_stride;
+
+    double pv[RV];
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < RV; ++r) {
+      const int col = c.pt_vn[vpos[r]];
+      pv[r] = (col >= c.punct) ? p0[col - c.punct] : 0.5;
+      ok = ok && fast_prior_ok(pv[r]);
+    }
+    // InitMsg: row slots and mirror slots (c2v = 0.5)
+    for (int e = tid; e < nslots; e += T) reinterpret_cast<double2 *>(smem)[e] = make_double2(0.5, 0.5);
+    if (__ballot(!ok) != 0 && (tid & 63) == 0)
+      __hip_atomic_fetch_or(&gs->nofast, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return;
+    const bool fast = fast_allowed && !ld_rlx(&gs->nofast);
+
+    int iter = 0;
+    bool conv = false;
+    bool alive;
+    if (fast)
+      alive = part_iterations<kG, RV, RC, RX, SYN, true>(a, c.M, c.N, NG, cw, gs, gen, same_xcd, abort, smem, dec,
+                                                         mb_v2c, mb_c2v, gc, vaddr, vpos, vact, pv, crow, cbase, ccol,
+                                                         cact, xr, xc, odd, member, iter, conv);
+    else
+      alive = part_iterations<kG, RV, RC, RX, SYN, false>(a, c.M, c.N, NG, cw, gs, gen, same_xcd, abort, smem, dec,
+                                                          mb_v2c, mb_c2v, gc, vaddr, vpos, vact, pv, crow, cbase,
+                                                          ccol, cact, xr, xc, odd, member, iter, conv);
+    if (!alive) return;
+
+    // ---- outputs: every member holds all hard decisions in LDS (dec) and
+    // writes its share; member 0 the scalars
+    if (a.iter_count > 0) {
+      if (a.uu_hat) {
+        uint8_t *u = a.uu_hat + (long long)cw * c.K;
+        const int lo = (int)((long long)c.K * member / kG), hi = (int)((long long)c.K * (member + 1) / kG);
+        for (int i = lo + tid; i < hi; i += T) u[i] = dec[c.pt_pos[i + c.info_off]];
+      }
+      if (a.cc_hat) {
+        uint8_t *o = a.cc_hat + (long long)cw * c.N;
+        for (int v = member * NG + tid; v < (member + 1) * NG; v += T) o[c.pt_vn[v]] = dec[v];
+      }
+      if (a.parity_cnt) {
+        int cnt = 0;
+#pragma unroll
+        for (int r = 0; r < RC; ++r) {
+          int p = 0;
+#pragma unroll
+          for (int k = 0; k < H; ++k) p ^= dec[ccol[r][k]];
+          const int full = p ^ swap_pair_i(p);
+          if (!odd && cact[r]) cnt += full;
+        }
+        if (cnt) __hip_atomic_fetch_add(&gs->pcnt, (unsigned)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (a.ref_bits) {
+        const uint64_t *ref = a.ref_bits + (long long)cw * c.Kw;
+        const int lo = (int)((long long)c.Kw * member / kG), hi = (int)((long long)c.Kw * (member + 1) / kG);
+        int errs = 0;
+        for (int w = lo + tid; w < hi; w += T) {
+          uint64_t word = 0;
+          const int base = w * 64;
+          const int nb = min(64, c.K - base);
+          for (int j = 0; j < nb; ++j) word |= (uint64_t)dec[c.pt_pos[c.info_off + base + j]] << j;
+          errs += __popcll(word ^ ref[w]);
+        }
+        if (errs) __hip_atomic_fetch_add(&gs->errs, (unsigned)errs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return;  // the members' sums are complete
+    if (member == 0 && tid == 0) {
+      const int errs = (int)ld_rlx(&gs->errs);
+      const int pcnt = (int)ld_rlx(&gs->pcnt);
+      if (a.ret) a.ret[cw] = iter + (iter < a.max_iter);
+      if (a.iters) a.iters[cw] = iter;
+      if (a.parity_cnt) a.parity_cnt[cw] = a.iter_count > 0 ? pcnt : 0;
+      if (a.cw_err && a.ref_bits) a.cw_err[cw] = a.iter_count > 0 ? errs : 0;
+      if (a.counters) {
+        const unsigned long long vn = conv ? (unsigned long long)iter + 1 : (unsigned long long)iter;
+        atomicAdd(&a.counters[CNT_VN_PHASES], vn);
+        atomicAdd(&a.counters[CNT_CN_PHASES], (unsigned long long)iter);
+        if (conv) atomicAdd(&a.counters[CNT_CONVERGED], 1ull);
+        if (a.ref_bits && a.iter_count > 0) {
+          atomicAdd(&a.counters[CNT_ERR_BIT], (unsigned long long)errs);
+          atomicAdd(&a.counters[CNT_ERR_BLK], errs > 0 ? 1ull : 0ull);
+          atomicAdd(&a.counters[CNT_TOT_BIT], (unsigned long long)c.K);
+          atomicAdd(&a.counters[CNT_TOT_BLK], 1ull);
+        }
+      }
+    }
+  }
+}
+
+template <int kG, int T, int RV, int RC, int RX, bool SYN>
+hipError_t launch_part_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast, int groups) {
+  auto kern = bp_part_kernel<kG, T, RV, RC, RX, SYN>;
+  const size_t lds = part_lds_bytes(c);
+  hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(a.queue, 0, sizeof(unsigned int), s);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(a.gsync, 0, sizeof(GroupSync) * (size_t)groups + sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
+  DevCode cc = c;
+  BpLaunch aa = a;
+  GroupSync *gs = reinterpret_cast<GroupSync *>(a.gsync);
+  uint8_t *gcch = a.gcch;
+  unsigned *abort = reinterpret_cast<unsigned *>(gs + groups);
+  unsigned int *q = a.queue;
+  int f = fast;
+  void *args[] = {&cc, &aa, &gs, &gcch, &abort, &q, &f};
+  return hipLaunchCooperativeKernel((const void *)kern, dim3((unsigned)(groups * kG)), dim3(T), args, (unsigned)lds,
+                                    s);
+}
+
 template <int kG, int T, int RV, int RC, bool SYN>
 hipError_t launch_coop_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast, int groups) {
   auto kern = bp_coop_kernel<kG, T, RV, RC, SYN>;
@@ -463,16 +874,26 @@ hipError_t launch_coop_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int
   return hipLaunchCooperativeKernel((const void *)kern, dim3((unsigned)(groups * kG)), dim3(T), args, 0, s);
 }
 
-// Tiling: KML_COOP = "G,T" (workgroups per codeword, threads per workgroup).
+// Kernel choice and tiling.  Default: the partitioned kernel (groups of 4,
+// KML_PART = threads per workgroup: 512, 768 or 1024) when the context built a
+// partition plan.  KML_COOP = "G,T" selects the global-slot kernel instead
+// (workgroups per codeword, threads per workgroup), for A/B measurements.
 struct CoopCfg {
+  bool part;
   int G, T;
 };
-CoopCfg coop_cfg() {
-  CoopCfg k{4, 512};
+CoopCfg coop_cfg(const DevCode &c) {
+  CoopCfg k{c.pt_G == kPartG && c.pt_vn != nullptr, 4, 512};
+  if (k.part) k.T = 1024;
   if (const char *e = getenv("KML_COOP")) {
     int g = 0, t = 0;
-    if (sscanf(e, "%d,%d", &g, &t) == 2 && (g == 4 || g == 8) && (t == 512 || t == 1024)) k = {g, t};
+    if (sscanf(e, "%d,%d", &g, &t) == 2 && (g == 4 || g == 8) && (t == 512 || t == 1024)) k = {false, g, t};
   }
+  if (k.part)
+    if (const char *e = getenv("KML_PART")) {
+      const int t = atoi(e);
+      if (t == 512 || t == 768 || t == 1024) k.T = t;
+    }
   return k;
 }
 
@@ -480,16 +901,35 @@ CoopCfg coop_cfg() {
 
 size_t bp_coop_sync_bytes(int groups) { return sizeof(GroupSync) * (size_t)groups + 64; }
 
+int bp_part_group_size(int N, int M, int E, int dv_max, int dc_max, int regular) {
+  if (!regular || dv_max != 3 || dc_max != 6 || (long long)E * 16 + 16 + N <= 160 * 1024) return 0;
+  if (N % kPartG || M % kPartG || (N / kPartG) % 16) return 0;
+  const int NG = N / kPartG, MG = M / kPartG;
+  // the largest tiling covers 2048 columns and half-rows per member; the LDS
+  // check including the mirror slots is part_plan_fits (after planning)
+  if ((long long)MG * 6 * 16 + N > 160 * 1024 || NG > 2048 || 2 * MG > 2048) return 0;
+  return kPartG;
+}
+
+bool part_plan_fits(int N, int M, int E, int ncut, int mirror_max, int xmax) {
+  const long long lds = ((long long)M / kPartG * 6 + mirror_max) * 16 + N;
+  return lds <= 160 * 1024 && 3LL * ncut <= 2LL * E && xmax <= 2 * 1024;
+}
+
 int bp_coop_groups(const DevCode &c) {
   if (!c.regular || !c.reg_pos || c.dv_max != 3 || c.dc_max != 6 || bp_uses_lds(c)) return 0;
-  const CoopCfg k = coop_cfg();
-  const int R = 8192 / (k.G * k.T);  // columns (and half-rows) per thread of the instantiated tilings
-  if ((c.N + k.G - 1) / k.G > R * k.T || (2 * c.M + k.G - 1) / k.G > R * k.T) return 0;
+  const CoopCfg k = coop_cfg(c);
+  if (!k.part) {
+    const int R = 8192 / (k.G * k.T);  // columns (and half-rows) per thread of the instantiated tilings
+    if ((c.N + k.G - 1) / k.G > R * k.T || (2 * c.M + k.G - 1) / k.G > R * k.T) return 0;
+  }
   int dev = 0, ncu = 0;
   hipGetDevice(&dev);
   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   return (ncu / (8 * k.G)) * 8;  // one workgroup per CU; 8 XCDs, groups of G per XCD
 }
+
+const char *bp_coop_family(const DevCode &c) { return coop_cfg(c).part ? "bp_part_kernel" : "bp_coop_kernel"; }
 
 hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s) {
   const int groups = bp_coop_groups(c);
@@ -497,7 +937,21 @@ hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s) {
   if (const char *k = getenv("KML_BP_KERNEL"))
     if (k[0] == 'g') return hipErrorNotSupported;
   const int fast = c.dv_max <= kFastMaxColumnDegree ? 1 : 0;
-  const CoopCfg k = coop_cfg();
+  const CoopCfg k = coop_cfg(c);
+  if (k.part) {
+    // exchange entries per thread: every member's lists must fit RX * T
+    int xmax = 0;
+    for (int m = 0; m < kPartG; m++) xmax = std::max(xmax, std::max(c.pt_xr_n[m], c.pt_xc_n[m]));
+#define KML_PART_CASE(T_, R_, X_)                                                                  \
+  if (k.T == T_ && xmax <= X_ * T_)                                                               \
+    return a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true>(c, a, s, fast, groups)             \
+                 : launch_part_t<kPartG, T_, R_, R_, X_, false>(c, a, s, fast, groups);
+    KML_PART_CASE(512, 4, 4)
+    KML_PART_CASE(768, 3, 3)
+    KML_PART_CASE(1024, 2, 2)
+#undef KML_PART_CASE
+    return hipErrorNotSupported;
+  }
 #define KML_COOP_CASE(G_, T_, R_)                                                                               \
   if (k.G == G_ && k.T == T_)                                                                                  \
     return a.syn ? launch_coop_t<G_, T_, R_, R_, true>(c, a, s, fast, groups)                                  \

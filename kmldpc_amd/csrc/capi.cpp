@@ -82,6 +82,7 @@ struct kml_ctx {
   DBuf d_queue, d_gslots, d_gsync, d_gcch;
   long long gslots_cap = 0;
   int coop_groups = 0;      // cooperative BP groups (0: kernel not used)
+  long long part_cut = 0;   // cut edges of the partition plan (partitioned cooperative kernel)
   bool coop_pending = false;  // a cooperative launch whose abort word is unchecked
   // workspaces
   DBuf w_y, w_h, w_h4, w_hhat, w_p0, w_uu, w_uh, w_uh4, w_ret, w_cch, w_syn, w_sel, w_met, w_pc, w_cnt, w_km, w_cwerr;
@@ -152,6 +153,22 @@ int upload_code(kml_ctx *c) {
   reserve(std::max<size_t>(L.enc_info.size(), 1) * 8);
   reserve(plan.c2v_addr.size() * 4);
   reserve(plan.pos.size() * 4);
+  // partition plan of the partitioned cooperative kernel (codes whose slots exceed one CU's LDS)
+  kml::PartitionPlan part;
+  const int part_G = kml::bp_part_group_size(L.N, L.M, L.E, L.dv_max, L.dc_max, regular);
+  if (part_G > 0 && !kml::plan_partition(L, part_G, part)) part.G = 0;
+  int part_xmax = 0;
+  for (int m = 0; part.G && m < part.G; m++)
+    part_xmax = std::max({part_xmax, part.xr_ptr[m + 1] - part.xr_ptr[m], part.xc_ptr[m + 1] - part.xc_ptr[m]});
+  if (part.G && !kml::part_plan_fits(L.N, L.M, L.E, part.ncut, part.mirror_max, part_xmax)) part.G = 0;
+  reserve(part.vn.size() * 4);
+  reserve(part.cn.size() * 4);
+  reserve(part.pos.size() * 4);
+  reserve(part.vaddr.size() * 4);
+  reserve(part.xr.size() * 4);
+  reserve(part.xr_ptr.size() * 4);
+  reserve(part.xc.size() * 4);
+  reserve(part.xc_ptr.size() * 4);
   HIPCHK(c, c->d_graph.ensure(bytes), "hipMalloc(graph)");
   std::vector<unsigned char> host(bytes, 0);
   auto put = [&](int i, const void *src, size_t n) {
@@ -166,6 +183,14 @@ int upload_code(kml_ctx *c) {
   put(6, L.enc_info.data(), L.enc_info.size() * 8);
   put(7, plan.c2v_addr.data(), plan.c2v_addr.size() * 4);
   put(8, plan.pos.data(), plan.pos.size() * 4);
+  put(9, part.vn.data(), part.vn.size() * 4);
+  put(10, part.cn.data(), part.cn.size() * 4);
+  put(11, part.pos.data(), part.pos.size() * 4);
+  put(12, part.vaddr.data(), part.vaddr.size() * 4);
+  put(13, part.xr.data(), part.xr.size() * 4);
+  put(14, part.xr_ptr.data(), part.xr_ptr.size() * 4);
+  put(15, part.xc.data(), part.xc.size() * 4);
+  put(16, part.xc_ptr.data(), part.xc_ptr.size() * 4);
   HIPCHK(c, hipMemcpy(c->d_graph.p, host.data(), bytes, hipMemcpyHostToDevice), "upload graph");
   unsigned char *base = c->d_graph.as<unsigned char>();
   kml::DevCode &d = c->dc;
@@ -178,6 +203,22 @@ int upload_code(kml_ctx *c) {
   d.enc_info = reinterpret_cast<const uint64_t *>(base + off[6]);
   d.reg_c2v = reg_T > 0 ? reinterpret_cast<const int32_t *>(base + off[7]) : nullptr;
   d.reg_pos = reinterpret_cast<const int32_t *>(base + off[8]);
+  d.pt_G = part.G;
+  d.pt_vn = part.G ? reinterpret_cast<const int32_t *>(base + off[9]) : nullptr;
+  d.pt_cn = part.G ? reinterpret_cast<const int32_t *>(base + off[10]) : nullptr;
+  d.pt_pos = part.G ? reinterpret_cast<const int32_t *>(base + off[11]) : nullptr;
+  d.pt_vaddr = part.G ? reinterpret_cast<const int32_t *>(base + off[12]) : nullptr;
+  d.pt_xr = part.G ? reinterpret_cast<const int32_t *>(base + off[13]) : nullptr;
+  d.pt_xr_ptr = part.G ? reinterpret_cast<const int32_t *>(base + off[14]) : nullptr;
+  d.pt_xc = part.G ? reinterpret_cast<const int32_t *>(base + off[15]) : nullptr;
+  d.pt_xc_ptr = part.G ? reinterpret_cast<const int32_t *>(base + off[16]) : nullptr;
+  d.pt_ncut = part.ncut;
+  d.pt_mirror = part.mirror_max;
+  for (int m = 0; m < 4; m++) {
+    d.pt_xr_n[m] = m < part.G ? part.xr_ptr[m + 1] - part.xr_ptr[m] : 0;
+    d.pt_xc_n[m] = m < part.G ? part.xc_ptr[m + 1] - part.xc_ptr[m] : 0;
+  }
+  c->part_cut = part.ncut;
   d.M = L.M;
   d.N = L.N;
   d.E = L.E;

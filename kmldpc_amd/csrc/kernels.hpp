@@ -27,6 +27,11 @@ struct DevCode {
   // not take that kernel.  vn_order then holds the planned column order.
   const int32_t *reg_c2v;  // aligned with col_slot: byte offset of the c2v message
   const int32_t *reg_pos;  // column -> position (index into the kernel's hard-decision bytes)
+  // Partition plan of the partitioned cooperative kernel (layout.hpp
+  // PartitionPlan); null / 0 when the code does not take it.
+  const int32_t *pt_vn, *pt_cn, *pt_pos, *pt_vaddr, *pt_xr, *pt_xr_ptr, *pt_xc, *pt_xc_ptr;
+  int pt_G, pt_ncut, pt_mirror;
+  int pt_xr_n[4], pt_xc_n[4];  // exchange-list lengths per member (host copy, launch checks)
 };
 
 // Counter block in device memory (uint64):
@@ -76,6 +81,14 @@ hipError_t launch_bp_irregular(const DevCode &c, const BpLaunch &a, hipStream_t 
 int bp_coop_groups(const DevCode &c);
 size_t bp_coop_sync_bytes(int groups);
 hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s);
+// Group size of the partitioned cooperative kernel (0: not used); host-side,
+// decides whether upload_code builds the partition plan.
+int bp_part_group_size(int N, int M, int E, int dv_max, int dc_max, int regular);
+// Does a partition plan (cut edges, most mirror slots of a member, longest
+// exchange list) fit the partitioned kernel's LDS, scratch and tilings?
+bool part_plan_fits(int N, int M, int E, int ncut, int mirror_max, int xmax);
+// Name of the cooperative kernel launch_bp_coop runs for this code.
+const char *bp_coop_family(const DevCode &c);
 bool bp_coop_aborted(const BpLaunch &a, int groups, hipStream_t s);
 // Threads per workgroup of the regular kernel for this code shape, 0 if it does
 // not apply (host-side; decides whether upload_code builds the LDS plan).

@@ -163,3 +163,178 @@ static void plan_uncached(const LdpcCode &L, RegularLayout &out) {
 }
 
 }  // namespace kml
+
+namespace kml {
+
+namespace {
+
+// Capacity-bounded majority assignment: every item goes to the part holding
+// most of its neighbours, strongest preferences first, each part taking at
+// most `cap` items (ties broken by a seeded random key).
+void assign_majority(const std::vector<int32_t> &ptr, const std::vector<int32_t> &nbr,
+                     const std::vector<int32_t> &nbr_part, int G, int cap, Xorshift &rng,
+                     std::vector<int32_t> &part) {
+  const int n = (int)ptr.size() - 1;
+  struct Cand {
+    int cnt;
+    uint32_t key;
+    int item, g;
+  };
+  std::vector<Cand> cand;
+  cand.reserve((size_t)n * G);
+  std::vector<int> cnt(G);
+  for (int i = 0; i < n; i++) {
+    std::fill(cnt.begin(), cnt.end(), 0);
+    for (int e = ptr[i]; e < ptr[i + 1]; e++) cnt[nbr_part[nbr[e]]]++;
+    for (int g = 0; g < G; g++) cand.push_back({cnt[g], (uint32_t)rng.next(), i, g});
+  }
+  std::sort(cand.begin(), cand.end(), [](const Cand &a, const Cand &b) {
+    return a.cnt != b.cnt ? a.cnt > b.cnt : a.key < b.key;
+  });
+  part.assign(n, -1);
+  std::vector<int> load(G, 0);
+  for (const Cand &c : cand)
+    if (part[c.item] < 0 && load[c.g] < cap) {
+      part[c.item] = c.g;
+      load[c.g]++;
+    }
+}
+
+}  // namespace
+
+bool plan_partition(const LdpcCode &L, int G, PartitionPlan &out) {
+  const int M = L.M, N = L.N, E = L.E;
+  if (G <= 0 || M % G || N % G || !L.dv_max || !L.dc_max) return false;
+  for (int j = 0; j < N; j++)
+    if (L.col_ptr[j + 1] - L.col_ptr[j] != L.dv_max) return false;
+  for (int i = 0; i < M; i++)
+    if (L.row_ptr[i + 1] - L.row_ptr[i] != L.dc_max) return false;
+  const int MG = M / G, NG = N / G, dc = L.dc_max, dv = L.dv_max;
+  // slot -> row
+  std::vector<int32_t> slot_row(E);
+  for (int i = 0; i < M; i++)
+    for (int e = L.row_ptr[i]; e < L.row_ptr[i + 1]; e++) slot_row[e] = i;
+  // column adjacency (rows) and row adjacency (columns)
+  std::vector<int32_t> col_rows(E), row_cols(L.row_col.begin(), L.row_col.end());
+  for (int e = 0; e < E; e++) col_rows[e] = slot_row[L.col_slot[e]];
+
+  // initial row parts: breadth-first order over the Tanner graph, cut in G runs
+  std::vector<int32_t> rpart(M, -1), cpart;
+  {
+    std::vector<int32_t> order;
+    order.reserve(M);
+    std::vector<char> seen_r(M, 0), seen_c(N, 0);
+    for (int s = 0; s < M; s++) {
+      if (seen_r[s]) continue;
+      size_t head = order.size();
+      order.push_back(s);
+      seen_r[s] = 1;
+      while (head < order.size()) {
+        const int r = order[head++];
+        for (int e = L.row_ptr[r]; e < L.row_ptr[r + 1]; e++) {
+          const int c = row_cols[e];
+          if (seen_c[c]) continue;
+          seen_c[c] = 1;
+          for (int f = L.col_ptr[c]; f < L.col_ptr[c + 1]; f++) {
+            const int r2 = col_rows[f];
+            if (!seen_r[r2]) {
+              seen_r[r2] = 1;
+              order.push_back(r2);
+            }
+          }
+        }
+      }
+    }
+    for (int k = 0; k < M; k++) rpart[order[k]] = (int32_t)((long long)k * G / M);
+  }
+  auto cut_of = [&](const std::vector<int32_t> &rp, const std::vector<int32_t> &cp) {
+    long long n = 0;
+    for (int j = 0; j < N; j++)
+      for (int e = L.col_ptr[j]; e < L.col_ptr[j + 1]; e++) n += rp[col_rows[e]] != cp[j];
+    return n;
+  };
+  Xorshift rng{0xC2B2AE3D27D4EB4Full};
+  long long best = -1;
+  std::vector<int32_t> best_r, best_c;
+  for (int it = 0; it < 40; it++) {
+    assign_majority(L.col_ptr, col_rows, rpart, G, NG, rng, cpart);
+    const long long cc = cut_of(rpart, cpart);
+    if (best < 0 || cc < best) {
+      best = cc;
+      best_r = rpart;
+      best_c = cpart;
+    }
+    assign_majority(L.row_ptr, row_cols, cpart, G, MG, rng, rpart);
+  }
+
+  // member orders: columns and rows by index
+  out.G = G;
+  out.MG = MG;
+  out.NG = NG;
+  out.vn.clear();
+  out.cn.clear();
+  for (int g = 0; g < G; g++) {
+    for (int j = 0; j < N; j++)
+      if (best_c[j] == g) out.vn.push_back(j);
+    for (int i = 0; i < M; i++)
+      if (best_r[i] == g) out.cn.push_back(i);
+  }
+  out.pos.assign(N, 0);
+  for (int p = 0; p < N; p++) out.pos[out.vn[p]] = p;
+  std::vector<int32_t> row_at(M);
+  for (int p = 0; p < M; p++) row_at[out.cn[p]] = p;
+  const int EG = MG * dc;
+
+  // cut edges, sorted by (row owner, column owner, partitioned row slot)
+  struct Cut {
+    int R, S, slot, col_pos, k;
+  };
+  std::vector<Cut> cuts;
+  for (int p = 0; p < N; p++) {
+    const int j = out.vn[p];
+    for (int e = L.col_ptr[j], k = 0; e < L.col_ptr[j + 1]; e++, k++) {
+      const int s = L.col_slot[e], r = slot_row[s];
+      if (best_r[r] != best_c[j]) cuts.push_back({best_r[r], best_c[j], row_at[r] * dc + (s - L.row_ptr[r]), p, k});
+    }
+  }
+  std::sort(cuts.begin(), cuts.end(), [](const Cut &a, const Cut &b) {
+    return a.R != b.R ? a.R < b.R : a.S != b.S ? a.S < b.S : a.slot < b.slot;
+  });
+  out.ncut = (int)cuts.size();
+  if (out.ncut >= (1 << 15)) return false;  // packed (x << 16) entries
+  std::vector<std::vector<int32_t>> xr(G), xc(G);
+  std::vector<int> mirror_of(cuts.size());
+  for (size_t x = 0; x < cuts.size(); x++) {
+    const Cut &c = cuts[x];
+    xr[c.R].push_back((int32_t)((x << 16) | (uint32_t)(c.slot - c.R * EG)));
+    mirror_of[x] = (int)xc[c.S].size();
+    xc[c.S].push_back((int32_t)((x << 16) | (uint32_t)(EG + mirror_of[x])));
+  }
+  out.mirror_max = 0;
+  out.xr.clear();
+  out.xc.clear();
+  out.xr_ptr.assign(1, 0);
+  out.xc_ptr.assign(1, 0);
+  for (int g = 0; g < G; g++) {
+    out.mirror_max = std::max(out.mirror_max, (int)xc[g].size());
+    if (EG + (int)xc[g].size() >= (1 << 16)) return false;
+    out.xr.insert(out.xr.end(), xr[g].begin(), xr[g].end());
+    out.xc.insert(out.xc.end(), xc[g].begin(), xc[g].end());
+    out.xr_ptr.push_back((int32_t)out.xr.size());
+    out.xc_ptr.push_back((int32_t)out.xc.size());
+  }
+  // per-edge LDS addresses of the VN phase: own row slot, or the mirror slot
+  out.vaddr.assign((size_t)N * dv, 0);
+  for (int p = 0; p < N; p++) {
+    const int j = out.vn[p], g = best_c[j];
+    for (int e = L.col_ptr[j], k = 0; e < L.col_ptr[j + 1]; e++, k++) {
+      const int s = L.col_slot[e], r = slot_row[s];
+      if (best_r[r] == g) out.vaddr[(size_t)p * dv + k] = ((row_at[r] - g * MG) * dc + (s - L.row_ptr[r])) * 16;
+    }
+  }
+  for (size_t x = 0; x < cuts.size(); x++)
+    out.vaddr[(size_t)cuts[x].col_pos * dv + cuts[x].k] = (EG + mirror_of[x]) * 16;
+  return true;
+}
+
+}  // namespace kml

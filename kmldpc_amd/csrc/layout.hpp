@@ -33,3 +33,38 @@ struct RegularLayout {
 void plan_regular_layout(const LdpcCode &L, int T, RegularLayout &out);
 
 }  // namespace kml
+
+namespace kml {
+
+// Partition plan for the partitioned cooperative BP kernel (bp_coop.hip,
+// bp_part_kernel): a group of G workgroups decodes one codeword; member m owns
+// the rows [m*MG, (m+1)*MG) and the columns [m*NG, (m+1)*NG) of the orders
+// below.  Its LDS holds the 16-byte slots of its rows (slot (P - m*MG)*dc + k
+// for the k-th edge of the row at plan index P) followed by one MIRROR slot per
+// CUT edge of its columns (an edge whose row another member owns).  Cut edges
+// are exchanged through two mailboxes in global memory, v2c (column owner ->
+// row owner) and c2v (row owner -> column owner), indexed by the cut-edge
+// index x, which is sorted by (row owner, column owner, row slot): each
+// sender's and each receiver's share is a few contiguous runs.  The planner
+// minimises the number of cut edges (balanced G-way partition of the Tanner
+// graph: alternating majority assignment of columns given rows and rows given
+// columns, capacity-bounded).  Any partition gives the same decoder output: it
+// only moves work between lanes.
+struct PartitionPlan {
+  int G = 0, MG = 0, NG = 0;
+  int ncut = 0;                 // cut edges (mailbox entries)
+  int mirror_max = 0;           // most mirror slots of one member
+  std::vector<int32_t> vn;      // N: columns in member order (member m: [m*NG, (m+1)*NG))
+  std::vector<int32_t> cn;      // M: rows in member order
+  std::vector<int32_t> pos;     // N: column -> index into vn
+  std::vector<int32_t> vaddr;   // 3N (dv = 3): [p*dv + k] = LDS byte offset of the k-th edge of column vn[p]
+                                // in its owner's LDS (a row slot or a mirror slot)
+  // exchange lists, per member [ptr[m], ptr[m+1]); entry = (x << 16) | (LDS slot index)
+  std::vector<int32_t> xr, xr_ptr;  // as row owner: cut edges of its rows
+  std::vector<int32_t> xc, xc_ptr;  // as column owner: cut edges of its columns (-> mirror slots)
+};
+
+// False when the code is not regular or M, N are not multiples of G.
+bool plan_partition(const LdpcCode &L, int G, PartitionPlan &out);
+
+}  // namespace kml

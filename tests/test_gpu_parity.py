@@ -327,9 +327,9 @@ def test_blind_gpu_monte_carlo(data_dir):
 
 CODES = [("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, 20),   # bp_regular_kernel (LDS)
          ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, 50),  # bp_irregular_kernel (LDS)
-         ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 20)]  # bp_coop_kernel (L2 slots)
+         ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 20)]  # bp_part_kernel (partitioned LDS slots)
 FAMILY = {"PEG2304regular0.5.txt": "bp_regular_kernel", "5GLDPCBG2a3_R12_K960.txt": "bp_irregular_kernel",
-          "PEG8064regular0.5.txt": "bp_coop_kernel"}
+          "PEG8064regular0.5.txt": "bp_part_kernel"}
 
 
 @pytest.mark.parametrize("matrix,modem,is5g,max_iter", CODES)
@@ -339,6 +339,21 @@ def test_dispatch_takes_the_specialised_kernel(data_dir, matrix, modem, is5g, ma
     ctx = ctx_for(data_dir, matrix, modem, is5g, max_iter)
     ctx.bp_decode(np.full((2, ctx.cc_len), 0.3), iter_count=2)
     assert ctx.bp_kernel() == FAMILY[matrix]
+
+
+def test_global_slot_cooperative_kernel_still_exact(data_dir, monkeypatch):
+    """KML_COOP=G,T selects the global-slot cooperative kernel (the partitioned
+    kernel's predecessor, kept for A/B): still bit-exact on PEG8064."""
+    monkeypatch.setenv("KML_COOP", "4,512")
+    ctx = ctx_for(data_dir, "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 20)
+    oc = oracle_for(data_dir, "PEG8064regular0.5.txt", False, 20)
+    rng = np.random.default_rng(21)
+    p0 = rng.uniform(0.1, 0.9, (5, ctx.cc_len))
+    r = ctx.bp_decode(p0, cc_hat=True)
+    assert ctx.bp_kernel() == "bp_coop_kernel"
+    for i in range(len(p0)):
+        ret, uh, cch, _ = oc.bp_decode(p0[i])
+        assert r["ret"][i] == ret and np.array_equal(r["cc_hat"][i], cch), i
 
 
 @pytest.mark.parametrize("matrix,modem,is5g,max_iter", CODES)
