@@ -42,3 +42,15 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all lib oracle clean
+
+# Phase-timing build of the partitioned cooperative kernel (s_memtime stamps,
+# kml_debug_part_stamps); load it with KML_LIB=kmldpc_amd/libkmldpc_amd_stamps.so
+STAMPS_LIB := kmldpc_amd/libkmldpc_amd_stamps.so
+STAMPS_OBJS := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(CPP_SRCS) $(filter-out bp_coop,$(HIP_SRCS)))) $(OBJDIR)/stamps/bp_coop.o
+$(OBJDIR)/stamps/bp_coop.o: $(CSRC)/bp_coop.hip $(HDRS)
+	@mkdir -p $(OBJDIR)/stamps
+	$(HIPCC) $(HIPFLAGS) -DKML_STAMPS=1 -c -o $@ $<
+$(STAMPS_LIB): $(STAMPS_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(STAMPS_OBJS) -Wl,-rpath,/opt/rocm/lib
+stamps: $(STAMPS_LIB)
+.PHONY: stamps

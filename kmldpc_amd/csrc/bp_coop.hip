@@ -52,6 +52,9 @@ struct GroupSync {
   unsigned errs;     // error bits of the codeword, summed over members
   unsigned pcnt;     // unsatisfied checks of the final hard decisions, summed
   unsigned xcc;      // bit per XCD a member runs on
+  // partitioned kernel: barrier counters by barrier parity, arrivals in the
+  // low 32 bits, parity-failure reports in the high 32 bits (part_barrier)
+  unsigned long long bar2[2];
 };
 
 constexpr int kPartG = 4;  // workgroups per codeword of the partitioned kernel
@@ -454,6 +457,85 @@ __global__ __launch_bounds__(T) void bp_coop_kernel(DevCode c, BpLaunch a, Group
   }
 }
 
+#ifdef KML_STAMPS
+// Phase timing of the partitioned kernel (a KML_STAMPS=1 build only): wave 0
+// of every workgroup adds s_memtime deltas per phase of its iterations.
+constexpr int kStampSlots = 10;
+__device__ unsigned long long kml_part_stamps[256 * kStampSlots];
+#define KML_STAMP(i)                                                                   \
+  do {                                                                                 \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                        \
+    if (threadIdx.x == 0 && blockIdx.x < 256)                                          \
+      atomicAdd(&kml_part_stamps[blockIdx.x * kStampSlots + (i)], _t - stamp_prev);    \
+    stamp_prev = _t;                                                                   \
+  } while (0)
+#else
+#define KML_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
+// Group barrier of the partitioned kernel, which also ORs the members'
+// early-stop flags: each member adds 1 + (its flag << 32) to the counter of
+// this barrier's parity (no member can reach the next barrier of the same
+// parity before every member has passed this one, so the value a poller sees
+// holds exactly this barrier's arrivals).  st (LDS, thread 0 only): expected
+// arrivals and flag totals seen, per parity.  Returns the number of members
+// that reported a flag, or -1 when the launch aborts.  The abort word is read
+// every 64 polls only, so a poll costs one L2 round trip.
+__device__ __forceinline__ unsigned long long ld_rlx64(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int kG>
+__device__ __forceinline__ int part_barrier(GroupSync *gs, unsigned long long *st, unsigned &nb, bool same_xcd,
+                                            unsigned *abort, int *flag) {
+  if (same_xcd)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else
+    __threadfence();
+  __syncthreads();
+  const int p = nb & 1;
+  ++nb;
+  __shared__ int res;
+  if (threadIdx.x == 0) {
+    if (!same_xcd) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    unsigned long long add = 1;
+    if (flag) {
+      if (*flag) add += 1ull << 32;
+      *flag = 0;  // the next reports follow this barrier
+    }
+    st[p] += kG;
+    __hip_atomic_fetch_add(&gs->bar2[p], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int r = 0;
+    unsigned long long v;
+    for (long long spin = 0;; ++spin) {
+      v = ld_rlx64(&gs->bar2[p]);
+      if ((unsigned)v >= (unsigned)st[p]) break;
+      if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
+        __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r = -1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (r == 0) {
+      const unsigned f = (unsigned)(v >> 32);
+      r = (int)(f - (unsigned)st[2 + p]);
+      st[2 + p] = f;
+    }
+    if (!same_xcd) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    res = r;
+  }
+  __syncthreads();
+  return res;
+}
+
 // ===========================================================================
 // Partitioned cooperative kernel (bp_part_kernel): the group mapping and the
 // group barriers above, but every message access of the arithmetic is an LDS
@@ -474,7 +556,8 @@ __global__ __launch_bounds__(T) void bp_coop_kernel(DevCode c, BpLaunch a, Group
 
 template <int kG, int RV, int RC, int RX, bool SYN, bool FAST>
 __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N, int NG, int cw, GroupSync *gs,
-                                                unsigned &gen, bool same_xcd, unsigned *abort, unsigned char *smem,
+                                                unsigned long long *bst, unsigned &nb, int *sfail, bool same_xcd,
+                                                unsigned *abort, unsigned char *smem,
                                                 uint8_t *dec, double2 *mb_v2c, double *mb_c2v, uint8_t *gc,
                                                 const int (&vaddr)[RV][3], const int (&vpos)[RV],
                                                 const bool (&vact)[RV], const double (&pv)[RV], const int (&crow)[RC],
@@ -486,7 +569,11 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
   double2 *slots = reinterpret_cast<double2 *>(smem);
   int iter = 0;
   bool conv = false;
+#ifdef KML_STAMPS
+  unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
+#endif
   for (; iter < a.iter_count; ++iter) {
+    KML_STAMP(0);  // iteration boundary
     // ---------------------------------- receive c2v of the cut edges (mirrors)
     if (iter > 0) {  // iteration 0 reads InitMsg's 0.5
 #pragma unroll
@@ -494,6 +581,7 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
         if (xc[q] >= 0) *reinterpret_cast<double *>(smem + (xc[q] & 0xFFFF) * 16) = ld_nt(&mb_c2v[xc[q] >> 16]);
       __syncthreads();
     }
+    KML_STAMP(1);  // receive c2v
     // ------------------------------------------------------------ VN phase
     __builtin_amdgcn_s_setprio(3);
     {
@@ -555,12 +643,15 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
         }
       }
     }
+    KML_STAMP(2);  // VN compute (wave 0)
     // ---------------------------------------------- send v2c of the cut edges
     __syncthreads();
+    KML_STAMP(3);  // VN drain (other waves)
 #pragma unroll
     for (int q = 0; q < RX; ++q)
       if (xc[q] >= 0) mb_v2c[xc[q] >> 16] = slots[xc[q] & 0xFFFF];
-    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return false;
+    if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return false;
+    KML_STAMP(4);  // send v2c + group barrier
 
     // ------------------- receive v2c and the other members' hard decisions
 #pragma unroll
@@ -574,6 +665,7 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
       *reinterpret_cast<u32x4 *>(dec + off) = v;
     }
     __syncthreads();
+    KML_STAMP(5);  // receive v2c + decisions
 
     // -------------------- early-stop parity check, folded into the CN barrier
     {
@@ -585,8 +677,7 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
         for (int k = 0; k < H; ++k) p ^= dec[ccol[r][k]];
         fail |= cact[r] ? (p ^ swap_pair_i(p)) : 0;
       }
-      if (__ballot(fail) != 0 && (tid & 63) == 0)
-        __hip_atomic_fetch_or(&gs->flag[iter & 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__ballot(fail) != 0 && (tid & 63) == 0) atomicOr(sfail, 1);  // reported at the CN barrier
     }
 
     // ------------------------------------------------------------ CN phase
@@ -644,18 +735,20 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
 #pragma unroll
       for (int r = 0; r < RC; ++r) syn0[r] = s0[r];
     }
+    KML_STAMP(6);  // parity + CN compute (wave 0)
     // ---------------------------------------------- send c2v of the cut edges
     __syncthreads();
+    KML_STAMP(7);  // CN drain (other waves)
 #pragma unroll
     for (int q = 0; q < RX; ++q)
       if (xr[q] >= 0) mb_c2v[xr[q] >> 16] = slots[xr[q] & 0xFFFF].x;
-    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return false;
-    if (!ld_rlx(&gs->flag[iter & 1])) {  // every row satisfied: stop before this CN phase
+    const int failing = part_barrier<kG>(gs, bst, nb, same_xcd, abort, sfail);
+    KML_STAMP(8);  // send c2v + group barrier
+    if (failing < 0) return false;
+    if (failing == 0) {  // every row satisfied: stop before this CN phase
       conv = true;
       break;
     }
-    if (member == 0 && tid == 0)  // cleared before anyone can OR into it (next VN barrier)
-      __hip_atomic_store(&gs->flag[(iter + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (SYN) {
 #pragma unroll
       for (int r = 0; r < RC; ++r)
@@ -719,12 +812,16 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     }
   }
 
-  unsigned gen = 0;
+  __shared__ unsigned long long bst[4];  // part_barrier state (thread 0)
+  __shared__ int sfail;                  // this member's early-stop flag (parity failures)
+  unsigned nb = 0;                       // barrier sequence number (uniform, same on every member)
   if (tid == 0) {
+    bst[0] = bst[1] = bst[2] = bst[3] = 0;
+    sfail = 0;
     const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
     __hip_atomic_fetch_or(&gs->xcc, 1u << xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (!group_barrier<kG>(gs, gen, false, abort)) return;
+  if (part_barrier<kG>(gs, bst, nb, false, abort, nullptr) < 0) return;
   const bool same_xcd = __popc(ld_rlx(&gs->xcc)) == 1;
 
   for (;;) {
@@ -733,10 +830,8 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
       __hip_atomic_store(&gs->nofast, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&gs->errs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&gs->pcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&gs->flag[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&gs->flag[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return;
+    if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;
     const int entry = (int)ld_rlx(&gs->cw);
     if (entry >= a.B) break;
     const int cw = a.cw_idx ? a.cw_idx[entry] : entry;
@@ -755,18 +850,18 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     for (int e = tid; e < nslots; e += T) reinterpret_cast<double2 *>(smem)[e] = make_double2(0.5, 0.5);
     if (__ballot(!ok) != 0 && (tid & 63) == 0)
       __hip_atomic_fetch_or(&gs->nofast, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return;
+    if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;
     const bool fast = fast_allowed && !ld_rlx(&gs->nofast);
 
     int iter = 0;
     bool conv = false;
     bool alive;
     if (fast)
-      alive = part_iterations<kG, RV, RC, RX, SYN, true>(a, c.M, c.N, NG, cw, gs, gen, same_xcd, abort, smem, dec,
+      alive = part_iterations<kG, RV, RC, RX, SYN, true>(a, c.M, c.N, NG, cw, gs, bst, nb, &sfail, same_xcd, abort, smem, dec,
                                                          mb_v2c, mb_c2v, gc, vaddr, vpos, vact, pv, crow, cbase, ccol,
                                                          cact, xr, xc, odd, member, iter, conv);
     else
-      alive = part_iterations<kG, RV, RC, RX, SYN, false>(a, c.M, c.N, NG, cw, gs, gen, same_xcd, abort, smem, dec,
+      alive = part_iterations<kG, RV, RC, RX, SYN, false>(a, c.M, c.N, NG, cw, gs, bst, nb, &sfail, same_xcd, abort, smem, dec,
                                                           mb_v2c, mb_c2v, gc, vaddr, vpos, vact, pv, crow, cbase,
                                                           ccol, cact, xr, xc, odd, member, iter, conv);
     if (!alive) return;
@@ -809,7 +904,7 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
         if (errs) __hip_atomic_fetch_add(&gs->errs, (unsigned)errs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return;  // the members' sums are complete
+    if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;  // the members' sums are complete
     if (member == 0 && tid == 0) {
       const int errs = (int)ld_rlx(&gs->errs);
       const int pcnt = (int)ld_rlx(&gs->pcnt);
@@ -928,6 +1023,19 @@ int bp_coop_groups(const DevCode &c) {
   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   return (ncu / (8 * k.G)) * 8;  // one workgroup per CU; 8 XCDs, groups of G per XCD
 }
+
+#ifdef KML_STAMPS
+}  // namespace kml
+extern "C" int kml_debug_part_stamps(unsigned long long *out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(kml::kml_part_stamps), sizeof(kml::kml_part_stamps));
+  if (reset) {
+    static unsigned long long zero[256 * kml::kStampSlots];
+    hipMemcpyToSymbol(HIP_SYMBOL(kml::kml_part_stamps), zero, sizeof(zero));
+  }
+  return e == hipSuccess ? 0 : -1;
+}
+namespace kml {
+#endif
 
 const char *bp_coop_family(const DevCode &c) { return coop_cfg(c).part ? "bp_part_kernel" : "bp_coop_kernel"; }
 
