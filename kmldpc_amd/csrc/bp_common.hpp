@@ -6,6 +6,25 @@ namespace kml {
 
 constexpr double kSmallestProb = 1.0e-12;  // lib/lab/include/utility.h:12
 
+// LDS accesses through precomputed 32-bit LDS addresses.  `smem + off` with a
+// runtime `off` makes hipcc emit a v_add_u32 of the dynamic-LDS base before
+// every ds_read / ds_write (it does not fold the base into the offset field);
+// a kernel that keeps absolute LDS addresses in its registers addresses with
+// the register directly.
+typedef __attribute__((address_space(3))) unsigned char lds_byte;
+typedef double dbl2 __attribute__((ext_vector_type(2)));  // 16-byte LDS slot (ds_write_b128)
+__device__ __forceinline__ unsigned lds_addr(const void *p) {
+  return (unsigned)(size_t)(const lds_byte *)p;
+}
+template <class T>
+__device__ __forceinline__ T lds_ld(unsigned a) {
+  return *(const __attribute__((address_space(3))) T *)(size_t)a;
+}
+template <class T>
+__device__ __forceinline__ void lds_st(unsigned a, T v) {
+  *(__attribute__((address_space(3))) T *)(size_t)a = v;
+}
+
 // q0 = n0 / s and q1 = n1 / s, both correctly rounded.
 //
 // FAST = false: two IEEE divisions.

@@ -23,10 +23,13 @@
 //     swap.
 //   * LDS placement (layout.hpp): the columns' lane assignment is annealed on
 //     the host against the VN phase's bank conflicts, the hard decisions are
-//     stored by lane position (contiguous byte stores), and a c2v message goes
-//     to the lower or upper half of its slot by bit 2 of the row's CN position,
-//     so that a 16-lane ds_write_b64 group of the CN phase hits 16 distinct
-//     bank pairs.  The VN phase reads it at the planned byte offset.
+//     stored by lane position (contiguous byte stores), rows are stored in CN
+//     position order with the lane pair's edges interleaved (the pair reads
+//     slots 2st, 2st+1 of its row at step st: a per-lane base register plus an
+//     immediate offset, conflict-free), and a c2v message goes to the lower or
+//     upper half of its slot by bit 2 of the row's CN position.  The VN phase
+//     reads it at the planned byte offset.
+//   * every LDS address is kept absolute in a register (bp_common.hpp lds_ld).
 #include "bp_common.hpp"
 #include "kernels.hpp"
 
@@ -47,12 +50,11 @@ __device__ __forceinline__ int swap_pair_i(int x) { return __builtin_amdgcn_mov_
 
 template <int T, int RV, int RC, int DV, int DC, bool SYN, bool FAST>
 __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, int cw, unsigned char *smem,
-                                           unsigned char *cch, const int (&vaddr)[RV][DV], const double (&pv)[RV],
-                                           const int (&crow)[RC], const int (&cbase)[RC],
-                                           const int (&ccol)[RC][(DC + 1) / 2], int odd, int chalf, int &iter_out,
+                                           unsigned hd, const unsigned (&vaddr)[RV][DV], const double (&pv)[RV],
+                                           const int (&crow)[RC], const unsigned (&rb)[RC], const unsigned (&rb2)[RC],
+                                           const unsigned (&wb)[RC],
+                                           const unsigned (&ccol)[RC][(DC + 1) / 2], int odd, int &iter_out,
                                            bool &conv_out) {
-  const int tid = threadIdx.x;
-  double2 *slots = reinterpret_cast<double2 *>(smem);
   static_assert(DC % 2 == 0, "the lane-pair split assumes an even row degree");
   constexpr int H = DC / 2;
   int iter = 0;
@@ -72,7 +74,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
 #pragma unroll
       for (int r = 0; r < RV; ++r)
 #pragma unroll
-        for (int k = 0; k < DV; ++k) c0s[r][k] = *reinterpret_cast<const double *>(smem + vaddr[r][k]);
+        for (int k = 0; k < DV; ++k) c0s[r][k] = lds_ld<double>(vaddr[r][k]);
       double a0[RV], a1[RV], al0[RV][DV], al1[RV][DV];
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
@@ -91,7 +93,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
           if (k + 1 < DV)
             div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r]);
           else  // the posterior only feeds the hard decision
-            cch[r * T + tid] = (unsigned char)hard_decision<FAST>(n0, n1);
+            lds_st<unsigned char>(hd + r * T, (unsigned char)hard_decision<FAST>(n0, n1));
         }
       double b0[RV], b1[RV];
 #pragma unroll
@@ -108,7 +110,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
           const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
           double q0, q1;
           div2<FAST>(t0, t1, t0 + t1, q0, q1);
-          *reinterpret_cast<double2 *>(smem + (vaddr[r][k] & ~8)) = make_double2(q0, q1);
+          lds_st<dbl2>(vaddr[r][k] & ~15u, dbl2{q0, q1});
           if (k > 0) {
             const double c0 = c0s[r][k];
             if (unit) {  // (c0, 1 - c0) / (c0 + (1 - c0)): the sum rounds to exactly 1 (bp_common.hpp)
@@ -129,7 +131,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
     for (int r = 0; r < RC; ++r) {
       int p = 0;
 #pragma unroll
-      for (int k = 0; k < H; ++k) p ^= cch[ccol[r][k]];
+      for (int k = 0; k < H; ++k) p ^= lds_ld<unsigned char>(ccol[r][k]);
       fail |= p ^ swap_pair_i(p);
     }
     // The OR over the workgroup is folded into the CN phase's closing barrier:
@@ -163,7 +165,9 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
         if (advance) {
 #pragma unroll
           for (int r = 0; r < RC; ++r) {
-            const double2 m = slots[cbase[r] + (odd ? DC - 1 - st : st)];
+            // edge (odd ? DC-1-st : st): physical slot 2st+odd of the row while
+            // st < H, 2(DC-1-st)+1-odd after (layout.cpp)
+            const dbl2 m = st < H ? lds_ld<dbl2>(rb[r] + st * 32) : lds_ld<dbl2>(rb2[r] + (DC - 1 - st) * 32);
             m0[r] = m.x;
             m1[r] = m.y;
           }
@@ -181,8 +185,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
             const bool unit = FAST && st == DC - 1;  // own state is the boundary (1, 0)
             const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
             const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
-            *reinterpret_cast<double *>(smem + (cbase[r] + (odd ? st : DC - 1 - st)) * 16 + chalf) =
-                clip_c2v<FAST>(div1<FAST>(t0, t0 + t1));
+            lds_st<double>(wb[r] + (DC - 1 - st) * 32, clip_c2v<FAST>(div1<FAST>(t0, t0 + t1)));
           }
         }
         if (advance) {
@@ -222,26 +225,38 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
   int *red = reinterpret_cast<int *>(smem + (size_t)c.E * 16);
   unsigned char *cch = smem + (size_t)c.E * 16 + kRedBytes;
 
-  int vcol[RV], vaddr[RV][DV];
+  const unsigned smem_a = lds_addr(smem), cch_a = lds_addr(cch);
+  int vcol[RV];
+  unsigned vaddr[RV][DV];
 #pragma unroll
   for (int r = 0; r < RV; ++r) {
     const int v = c.vn_order[r * T + tid];
     const int b = c.col_ptr[v];
     vcol[r] = v;
 #pragma unroll
-    for (int k = 0; k < DV; ++k) vaddr[r][k] = c.reg_c2v[b + k];
+    for (int k = 0; k < DV; ++k) {
+      vaddr[r][k] = smem_a + (unsigned)c.reg_c2v[b + k];
+      asm volatile("" : "+v"(vaddr[r][k]));
+    }
   }
   const int chalf = ((tid >> 3) & 1) * 8;  // bit 2 of the CN position (tid >> 1)
-  int crow[RC], cbase[RC], ccol[RC][H];
+  int crow[RC], cbase[RC];
+  unsigned rb[RC], rb2[RC], wb[RC], ccol[RC][H];
 #pragma unroll
   for (int r = 0; r < RC; ++r) {
     const int row = c.cn_order[r * (T / 2) + (tid >> 1)];
     crow[r] = row;
     cbase[r] = c.row_ptr[row];
+    // the row's slots sit at its CN position, the pair's edges interleaved (layout.cpp)
+    rb[r] = smem_a + (unsigned)((r * (T / 2) + (tid >> 1)) * DC + odd) * 16;
+    rb2[r] = rb[r] + 16 - 32 * odd;
+    wb[r] = rb[r] + chalf;
+    asm volatile("" : "+v"(rb[r]), "+v"(rb2[r]), "+v"(wb[r]));
 #pragma unroll
     for (int k = 0; k < H; ++k) {  // parity columns: even lane edges [0, DC/2), odd lane [DC/2, DC)
       const int e = odd ? DC / 2 + k : k;
-      ccol[r][k] = c.reg_pos[c.row_col[cbase[r] + (e < DC ? e : DC - 1)]];
+      ccol[r][k] = cch_a + (unsigned)c.reg_pos[c.row_col[cbase[r] + (e < DC ? e : DC - 1)]];
+      asm volatile("" : "+v"(ccol[r][k]));  // keep the absolute address (no base re-add per use)
     }
   }
 
@@ -272,10 +287,10 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
     int iter = 0;
     bool conv = false;
     if (fast)
-      decode_reg<T, RV, RC, DV, DC, SYN, true>(c, a, cw, smem, cch, vaddr, pv, crow, cbase, ccol, odd, chalf, iter,
+      decode_reg<T, RV, RC, DV, DC, SYN, true>(c, a, cw, smem, cch_a + tid, vaddr, pv, crow, rb, rb2, wb, ccol, odd, iter,
                                               conv);
     else
-      decode_reg<T, RV, RC, DV, DC, SYN, false>(c, a, cw, smem, cch, vaddr, pv, crow, cbase, ccol, odd, chalf, iter,
+      decode_reg<T, RV, RC, DV, DC, SYN, false>(c, a, cw, smem, cch_a + tid, vaddr, pv, crow, rb, rb2, wb, ccol, odd, iter,
                                                conv);
 
     if (a.iter_count > 0) {
@@ -293,7 +308,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
         for (int r = 0; r < RC; ++r) {
           int p = 0;
 #pragma unroll
-          for (int k = 0; k < H; ++k) p ^= cch[ccol[r][k]];
+          for (int k = 0; k < H; ++k) p ^= lds_ld<unsigned char>(ccol[r][k]);
           const int full = p ^ swap_pair_i(p);
           if (!odd) cnt += full;
         }

@@ -58,11 +58,23 @@ static void plan_uncached(const LdpcCode &L, RegularLayout &out) {
   // CN position of each row -> half bit h(row) = (position >> 2) & 1
   std::vector<int> row_pos(L.M);
   for (int i = 0; i < L.M; i++) row_pos[L.cn_order[i]] = i;
-  std::vector<int> slot_h(L.E);
+  // Physical slot of the j-th edge of a row (row_ptr order): rows are stored in
+  // CN position order, and within a row the edges the even lane reads
+  // (j < dc/2, ascending) and the odd lane reads (j >= dc/2, descending)
+  // alternate, so at step st the pair reads slots 2st and 2st+1 of its row
+  // (slots 2(dc-1-st)+1 and 2(dc-1-st) once st >= dc/2): per-lane base registers
+  // plus immediate offsets, and conflict-free ds_read_b128 / ds_write_b64 groups
+  // (consecutive positions).
+  const int dc = L.dc_max;
+  std::vector<int> slot_h(L.E), phys(L.E);
   for (int i = 0; i < L.M; i++)
-    for (int e = L.row_ptr[i]; e < L.row_ptr[i + 1]; e++) slot_h[e] = (row_pos[i] >> 2) & 1;
+    for (int e = L.row_ptr[i]; e < L.row_ptr[i + 1]; e++) {
+      const int j = e - L.row_ptr[i];
+      slot_h[e] = (row_pos[i] >> 2) & 1;
+      phys[e] = row_pos[i] * dc + (j < dc / 2 ? 2 * j : 2 * (dc - 1 - j) + 1);
+    }
   out.c2v_addr.resize(L.E);
-  for (int e = 0; e < L.E; e++) out.c2v_addr[e] = L.col_slot[e] * 16 + 8 * slot_h[L.col_slot[e]];
+  for (int e = 0; e < L.E; e++) out.c2v_addr[e] = phys[L.col_slot[e]] * 16 + 8 * slot_h[L.col_slot[e]];
 
   // bank bins per (column, k): ds_write_b128 of the slot (8-lane groups, 8 bins
   // of 16 B mod 128 B) and ds_read_b64 of the c2v half (32-lane halves, 32 bins
@@ -72,7 +84,7 @@ static void plan_uncached(const LdpcCode &L, RegularLayout &out) {
     for (int k = 0; k < dv; k++) {
       const int e = L.col_ptr[j] + std::min(k, L.col_ptr[j + 1] - L.col_ptr[j] - 1);
       const int a = out.c2v_addr[e];
-      wb[(size_t)j * dv + k] = (uint8_t)((L.col_slot[e]) & 7);
+      wb[(size_t)j * dv + k] = (uint8_t)((a >> 4) & 7);
       rb[(size_t)j * dv + k] = (uint8_t)((a >> 3) & 31);
     }
 
