@@ -18,6 +18,8 @@
 // reference's order; exp() is kml_exp, a bit-exact restatement of the glibc exp
 // the reference calls (the ROCm device exp differs from it in the last bit on
 // ~6% of inputs), so P0 is bit-identical to the CPU path.
+#include <algorithm>
+
 #include "demap_common.hpp"
 #include "kernels.hpp"
 
@@ -30,40 +32,81 @@ __global__ __launch_bounds__(256) void demap_kernel(const double *__restrict__ c
                                                     int S, int reps, const double2 *__restrict__ h, int h_stride,
                                                     const int32_t *__restrict__ h_sel, double var, int B,
                                                     double *__restrict__ p0) {
-  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (long long)B * S) return;
-  const int ent = (int)(gid / S);
-  const int j = (int)(gid - (long long)ent * S);
-  const double2 hh = h[(long long)ent * h_stride + (h_sel ? h_sel[ent] : 0)];
-  const double2 yy = y[(long long)(ent / reps) * S + j];
-  double out[MB];
-  demap_symbol<MB>(cons, yy.x, yy.y, hh.x, hh.y, var, out);
+  __shared__ double cl[2 << MB];  // the constellation, read with uniform LDS loads
+  __shared__ uint64_t etab[256];
+  for (int k = threadIdx.x; k < (2 << MB); k += blockDim.x) cl[k] = cons[k];
+  stage_exp_table(etab);
+  __syncthreads();
+  // grid-stride over the symbols: the LDS staging above is paid once per
+  // workgroup, not once per 256 symbols
+  const long long n = (long long)B * S;
+  for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < n;
+       gid += (long long)gridDim.x * blockDim.x) {
+    const int ent = (int)(gid / S);
+    const int j = (int)(gid - (long long)ent * S);
+    const double2 hh = h[(long long)ent * h_stride + (h_sel ? h_sel[ent] : 0)];
+    const double2 yy = y[(long long)(ent / reps) * S + j];
+    double out[MB];
+    demap_symbol<MB>((lds_cons)cl, (lds_exptab)etab, yy.x, yy.y, hh.x, hh.y, var, out);
 #pragma unroll
-  for (int j = 0; j < MB; ++j) p0[gid * MB + j] = out[j];
+    for (int b = 0; b < MB; ++b) p0[gid * MB + b] = out[b];
+  }
 }
 
-// One workgroup per codeword: hard decisions of the 4 candidates into LDS,
-// then the unsatisfied-check counts.
+// One workgroup per codeword: hard decisions of the candidates into LDS, then
+// the unsatisfied-check counts.  The (candidate, symbol) pairs are flattened
+// over the workgroup; each symbol's decisions come from the single-precision
+// screen (hard_bits_screen) unless a bit is too close to call, in which case
+// the exact demapper decides.
 template <int MB>
-__global__ __launch_bounds__(256) void cand_metric_kernel(DevCode c, const double *__restrict__ cons,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? 3 : 1))) void cand_metric_kernel(DevCode c, const double *__restrict__ cons,
                                                           const double2 *__restrict__ y, int S,
                                                           const double2 *__restrict__ h4, int nc, double var,
-                                                          double *__restrict__ metrics, int32_t *__restrict__ chosen) {
+                                                          double inv_var, double *__restrict__ metrics,
+                                                          int32_t *__restrict__ chosen) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int *cnt = reinterpret_cast<int *>(smem);  // 4 counters
-  unsigned char *hb = smem + 16;             // [4][cc_len]
+  int *cnt = reinterpret_cast<int *>(smem);  // 4 counters + the undecided flag
+  unsigned char *hb = smem + 32;             // [4][cc_len]
+  constexpr bool kRescan = MB >= 5;
   const int cw = blockIdx.x;
   const int tid = threadIdx.x;
-  if (tid < 4) cnt[tid] = 0;
+  __shared__ double cl[2 << MB];
+  __shared__ uint64_t etab[256];
+  for (int k = tid; k < (2 << MB); k += blockDim.x) cl[k] = cons[k];
+  stage_exp_table(etab);
+  if (tid < 5) cnt[tid] = 0;
+  __syncthreads();
   const double2 *yy = y + (long long)cw * S;
-  for (int j = tid; j < S; j += blockDim.x) {
+  for (int i = tid; i < nc * S; i += blockDim.x) {
+    const int q = i / S, j = i - q * S;
     const double2 v = yy[j];
+    const double2 hh = h4[(long long)cw * nc + q];
+    unsigned bits;
+    if (!hard_bits_screen<MB>((lds_cons)cl, v.x, v.y, hh.x, hh.y, inv_var, bits)) {
+      if (kRescan) {
+        hb[q * c.cc_len + j * MB] = 2;  // undecided: the exact pass below
+        cnt[4] = 1;
+        continue;
+      }
+      double out[MB];
+      demap_symbol<MB>((lds_cons)cl, (lds_exptab)etab, v.x, v.y, hh.x, hh.y, var, out);
+      bits = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (q >= nc) break;
+      for (int b = 0; b < MB; ++b) bits |= (out[b] > 0.5 ? 1u : 0u) << b;  // kmcodec.cc:111-115
+    }
+#pragma unroll
+    for (int b = 0; b < MB; ++b) hb[q * c.cc_len + j * MB + b] = (bits >> b) & 1;
+  }
+  __syncthreads();
+  if (kRescan && cnt[4]) {  // 64QAM: the exact demapper in a pass of its own
+                            // keeps its registers out of the screening loop's
+    for (int i = tid; i < nc * S; i += blockDim.x) {
+      const int q = i / S, j = i - q * S;
+      if (hb[q * c.cc_len + j * MB] != 2) continue;
+      const double2 v = yy[j];
       const double2 hh = h4[(long long)cw * nc + q];
       double out[MB];
-      demap_symbol<MB>(cons, v.x, v.y, hh.x, hh.y, var, out);
+      demap_symbol<MB>((lds_cons)cl, (lds_exptab)etab, v.x, v.y, hh.x, hh.y, var, out);
 #pragma unroll
       for (int b = 0; b < MB; ++b) hb[q * c.cc_len + j * MB + b] = out[b] > 0.5 ? 1 : 0;  // kmcodec.cc:111-115
     }
@@ -192,7 +235,13 @@ hipError_t launch_demap(int bits, const double *cons, const double2 *y, int S, i
                         int h_stride, const int32_t *h_sel, double var, int B, double *p0, hipStream_t s) {
   const long long n = (long long)B * S;
   if (n == 0) return hipSuccess;
-  const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
+  int dev = 0, ncu = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  // small constellations: 8 workgroups per CU, grid-stride; 64QAM (three
+  // waves per SIMD, long symbols): one symbol per thread
+  const long long wg = (n + 255) / 256;
+  const dim3 grid((unsigned)(bits >= 5 ? wg : std::min<long long>(wg, 8LL * ncu))), blk(256);
   switch (bits) {
     case 1: hipLaunchKernelGGL(demap_kernel<1>, grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0); break;
     case 2: hipLaunchKernelGGL(demap_kernel<2>, grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0); break;
@@ -209,7 +258,7 @@ hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, co
                               hipStream_t s) {
   if (B == 0) return hipSuccess;
   if (nc < 1 || nc > 4) return hipErrorInvalidValue;
-  const size_t lds = 16 + 4 * (size_t)c.cc_len;
+  const size_t lds = 32 + 4 * (size_t)c.cc_len;
   const dim3 grid(B), blk(256);
   switch (bits) {
 #define KML_CM(MBV)                                                                                          \
@@ -217,7 +266,8 @@ hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, co
     hipError_t e = hipFuncSetAttribute((const void *)cand_metric_kernel<MBV>,                                \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
     if (e != hipSuccess) return e;                                                                           \
-    hipLaunchKernelGGL(cand_metric_kernel<MBV>, grid, blk, lds, s, c, cons, y, S, h4, nc, var, metrics, chosen); \
+    hipLaunchKernelGGL(cand_metric_kernel<MBV>, grid, blk, lds, s, c, cons, y, S, h4, nc, var, 1.0 / var, metrics, \
+                       chosen);                                                                              \
     break;                                                                                                   \
   }
     KML_CM(1)

@@ -17,13 +17,82 @@ __device__ __forceinline__ double prob_clip(double v) {  // utility.cc:18-26
   return v;
 }
 
-// P0 for the MB bits of one symbol.
-template <int MB>
-__device__ __forceinline__ void demap_symbol(const double *__restrict__ cons, double yr, double yi, double hr, double hi,
-                                             double var, double *out) {
+// Quotient n / s from a refined reciprocal r of s: div2's FAST sequence
+// (bp_common.hpp), bit-identical to an IEEE division when s is normal, n is 0
+// or at least 2^-969, the quotient is normal and the exponent gap is below 768.
+__device__ __forceinline__ double rcp_refine(double s) {
+  const double ns = -s;
+  double r = __builtin_amdgcn_rcp(s);
+  double e = fma(ns, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(ns, r, 1.0);
+  return fma(r, e, r);
+}
+__device__ __forceinline__ double qdiv(double n, double s, double r) {
+  const double m = n * r;
+  return fma(fma(-s, m, n), r, m);
+}
+
+// Constellation points staged in LDS by the calling kernel (cons_lds); CP is
+// the pointer type the demap helpers read them through.
+typedef const __attribute__((address_space(3))) double *lds_cons;
+
+// The exp table (kExpTabDev, 128 (tail, scale bits) pairs) staged in LDS by the
+// calling kernel: one ds_read_b128 per exp instead of two scattered global loads.
+typedef const __attribute__((address_space(3))) uint64_t *lds_exptab;
+__device__ __forceinline__ void stage_exp_table(uint64_t *dst) {  // dst: a __shared__ array
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) dst[i] = kExpTabDev[i];
+}
+
+// glibc's exp (kml_exp_t<true>) on its main path only: exact for x == 0 and
+// for 2^-54 <= |x| < 512, where glibc takes no special case (x == 0 gives
+// fma(1, 0, 1) = 1 here, as glibc's 1 + x).  exp_core_ok says whether x is in
+// that domain; callers fall back to kml_exp outside it.
+__device__ __forceinline__ bool exp_core_ok(double x) {
+  const double a = fabs(x);  // branch-free: (2^-54 <= |x| < 512) or x == 0
+  return (a >= 0x1p-54) & (a < 512.0) | (x == 0.0);
+}
+__device__ __forceinline__ double exp_core(double x, lds_exptab tab) {
+  const double InvLn2N = 0x1.71547652b82fep0 * 128;
+  const double Shift = 0x1.8p52;
+  const double NegLn2hiN = -0x1.62e42fefa0000p-8;
+  const double NegLn2loN = -0x1.cf79abc9e3b3ap-47;
+  const double C2 = 0x1.ffffffffffdbdp-2, C3 = 0x1.555555555543cp-3;
+  const double C4 = 0x1.55555cf172b91p-5, C5 = 0x1.1111167a4d017p-7;
+  double kd = fma(InvLn2N, x, Shift);
+  const uint64_t ki = as_u64(kd);
+  kd -= Shift;
+  const double r = fma(kd, NegLn2loN, fma(kd, NegLn2hiN, x));
+  const int idx = (int)(2 * (ki % 128));
+  const double tail = as_f64(tab[idx]);
+  const uint64_t sbits = tab[idx + 1] + (ki << (52 - 7));
+  const double r2 = r * r;
+  const double tmp = fma(r2 * r2, fma(r, C5, C4), fma(r2, fma(r, C3, C2), tail + r));
+  const double scale = as_f64(sbits);
+  return fma(scale, tmp, scale);
+}
+
+// P0 for the MB bits of one symbol.  FAST: the divisions by var, by the
+// exponential sum, by the prior-weighted sum and by q0 + q1 share one
+// reciprocal refinement each (qdiv); returns false, with out[] unset, when an
+// operand leaves the range where that is exact, and the caller reruns the
+// symbol with IEEE divisions (FAST = false, always true).  The ranges:
+//   * var in [2^-64, 2^64] and every squared distance n_k in [2^-512, 2^512]:
+//     n_k / var is exact (n_k = 0, a symbol exactly on a point, falls back);
+//   * the exponential sum lies in [1, KC] (its largest term is exp(0) = 1);
+//     a term below 2^-969 divides inexactly, but its quotient and the IEEE one
+//     are both far below 1e-12, so ProbClip maps both to 1e-12;
+//   * the weighted sum in [2^-64, 2^64] (it is at least w / KC): the clipped
+//     terms (>= w * 1e-12) divide exactly, and so do q0 and q1 (>= 1e-14,
+//     q0 + q1 ~ 2).
+template <int MB, bool FAST, class CP>
+__device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double yr, double yi, double hr,
+                                               double hi, double var, double *out) {
   constexpr int KC = 1 << MB;
   double pr[KC];
   double mx = 0.0;
+  double nmin = 0.0, nmax = 0.0, rv = 0.0;
+  if (FAST) rv = rcp_refine(var);
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
     const double cr = cons[2 * k], ci = cons[2 * k + 1];
@@ -31,29 +100,51 @@ __device__ __forceinline__ void demap_symbol(const double *__restrict__ cons, do
     double si = cr * hi + ci * hr;
     sr = sr - yr;  // symbol -= yy
     si = si - yi;
-    const double d = (sr * sr + si * si) / var;
+    const double n = sr * sr + si * si;
+    double d;
+    if (FAST) {
+      nmin = k == 0 ? n : fmin(nmin, n);
+      nmax = k == 0 ? n : fmax(nmax, n);
+      d = qdiv(n, var, rv);
+    } else {
+      d = n / var;
+    }
     pr[k] = -d;
     if (k == 0 || mx < pr[k]) mx = pr[k];  // *max_element
   }
+  if (FAST && !(nmin >= 0x1p-512 && nmax <= 0x1p512 && var >= 0x1p-64 && var <= 0x1p64)) return false;
   double sum = 0.0;
+  bool eok = true;
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
-    pr[k] = kml_exp(pr[k] - mx);  // glibc exp, bit-exact (exact_math.hpp)
+    const double x = pr[k] - mx;
+    if (FAST) {  // glibc's main path (exp_core), the rest falls back
+      eok &= exp_core_ok(x);
+      pr[k] = exp_core(x, etab);
+    } else {
+      pr[k] = kml_exp(x);  // glibc exp, bit-exact (exact_math.hpp)
+    }
     sum += pr[k];
   }
+  if (FAST && !(eok && sum >= 1.0 && sum <= (double)KC)) return false;
   // normalise + ProbClip (modemlinearsystem.cc:240-246), ProbClip again (modem.cc:27)
   double w = 1.0;  // prod over bits of bitLin (= 0.5) or 1 - bitLin (= 0.5)
 #pragma unroll
   for (int j = 0; j < MB; ++j) w *= 0.5;
+  const double rs = FAST ? rcp_refine(sum) : 0.0;
   double sum2 = 0.0;
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
-    pr[k] = prob_clip(prob_clip(pr[k] / sum));
+    pr[k] = prob_clip(prob_clip(FAST ? qdiv(pr[k], sum, rs) : pr[k] / sum));
     pr[k] = w * pr[k];
     sum2 += pr[k];
   }
+  if (FAST && !(sum2 >= 0x1p-64 && sum2 <= 0x1p64)) return false;
+  const double rs2 = FAST ? rcp_refine(sum2) : 0.0;
 #pragma unroll
-  for (int k = 0; k < KC; ++k) pr[k] /= sum2;
+  for (int k = 0; k < KC; ++k) pr[k] = FAST ? qdiv(pr[k], sum2, rs2) : pr[k] / sum2;
+  // per-bit sums in ascending k (modem.cc:58-70); one bit at a time keeps two
+  // accumulators live next to the KC probabilities
 #pragma unroll
   for (int j = 0; j < MB; ++j) {
     double q0 = 0.0, q1 = 0.0;
@@ -66,9 +157,94 @@ __device__ __forceinline__ void demap_symbol(const double *__restrict__ cons, do
     }
     q0 /= 0.5;
     q1 /= (1.0 - 0.5);
-    out[j] = prob_clip(q0 / (q0 + q1));
+    const double t = q0 + q1;
+    out[j] = prob_clip(FAST ? qdiv(q0, t, rcp_refine(t)) : q0 / t);
+  }
+  return true;
+}
+
+template <int MB, class CP>
+__device__ __forceinline__ void demap_symbol(CP cons, lds_exptab etab, double yr, double yi, double hr, double hi,
+                                             double var, double *out) {
+  // 64QAM: the fast path's live state exceeds the 168 registers of three
+  // waves per SIMD (the compiler then runs one wave); the IEEE path fits
+  if (MB >= 5 || !demap_symbol_t<MB, true>(cons, etab, yr, yi, hr, hi, var, out)) {
+    // rare: reload the constellation rather than keep the fast path's loads
+    // live across it (they would pin 4 * KC registers)
+    asm volatile("" : "+v"(cons));
+    demap_symbol_t<MB, false>(cons, etab, yr, yi, hr, hi, var, out);
   }
 }
 
+// Hard decisions rr_j = (P0_j > 0.5) of one symbol's MB bits (the metric's
+// kmcodec.cc:111-115) screened in single precision: returns false when some bit
+// is too close to call, and the caller then runs the exact demap_symbol.
+// P0_j > 0.5 iff q0_j > q1_j, where q_b = sum over the points whose label bit j
+// is b of c_k = ProbClip(exp(a_k) / sum exp(a)), a_k = dmin - d_k (the common
+// factors w and 1 / sum2 cancel, and ProbClip of the final quotient does not
+// move it across 0.5).  Here a_k is formed in double (d_k = n_k * (1/var),
+// 2^-52 relative), rounded to float (|a_k| <= 40: 2.4e-6 absolute), and
+// exp(a_k) = v_exp_f32(a_k * log2 e) (3.5e-6 absolute in the exponent, 1 ulp);
+// terms with a_k <= -40 are 0 here and below 4.3e-18 exactly, so both clip to
+// 1e-12.  Each c_k is then within 1e-5 relative of the reference's, the
+// sums q within 1.5e-5, and the reference's own rounding is below 1e-13: a bit
+// is decided only when one sum exceeds the other by 2^-12 (2.4e-4) relative.
+template <int MB, class CP>
+__device__ __forceinline__ bool hard_bits_screen(CP cons, double yr, double yi, double hr,
+                                                 double hi, double inv_var, unsigned &bits) {
+  constexpr int KC = 1 << MB;
+  // for large constellations d_k is computed twice (for dmin, then for a_k)
+  // rather than kept: KC doubles would cost 2 KC registers
+  auto dist = [&](int k) {
+    const double cr = cons[2 * k], ci = cons[2 * k + 1];
+    const double sr = cr * hr - ci * hi - yr;
+    const double si = cr * hi + ci * hr - yi;
+    return (sr * sr + si * si) * inv_var;
+  };
+  constexpr bool kRecompute = KC >= 32;
+  double dk[kRecompute ? 1 : KC];
+  double dmin = 0.0;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const double d = dist(k);
+    if (!kRecompute) dk[k] = d;
+    dmin = k == 0 ? d : fmin(dmin, d);
+  }
+  if (kRecompute) asm volatile("" : "+v"(cons));  // reload the points (no CSE across the passes)
+  float e[KC];
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const float a = (float)(dmin - (kRecompute ? dist(k) : dk[k]));
+    e[k] = a > -40.f ? __builtin_amdgcn_exp2f(a * 1.44269504f) : 0.f;
+    sum += e[k];
+  }
+  const float inv = 1.f / sum;
+  float q0[MB], q1[MB];
+#pragma unroll
+  for (int j = 0; j < MB; ++j) q0[j] = q1[j] = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const float c = fminf(fmaxf(e[k] * inv, 1e-12f), 1.f);
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      if (((k >> (MB - 1 - j)) & 1) == 0)
+        q0[j] += c;
+      else
+        q1[j] += c;
+    }
+  }
+  constexpr float g = 1.f + 0x1p-12f;
+  unsigned b = 0;
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    if (q0[j] > q1[j] * g)
+      b |= 1u << j;
+    else if (!(q1[j] > q0[j] * g))
+      return false;
+  }
+  bits = b;
+  return true;
+}
 
 }  // namespace kml

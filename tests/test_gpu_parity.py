@@ -189,6 +189,59 @@ def test_demap_vs_oracle(data_dir, matrix, modem, is5g, snr, n):
     assert np.array_equal(got, ref)
 
 
+def _adversarial_symbols(pts, S, B, rng):
+    """Received symbols that stress the demapper's fast-division ranges and the
+    metric's single-precision screen: exactly on a point (distance 0), on the
+    midpoint of two points and at 0 (P0 = 0.5 ties), tiny offsets, far outside
+    the constellation (exp underflow), with unit, rotated, tiny and huge
+    channels."""
+    y = np.zeros((B, S, 2))
+    th = np.zeros((B, 2))
+    for b in range(B):
+        h = [[1.0, 0.0], [0.0, 1.0], [0.6, -0.8], [1e-3, 2e-3], [40.0, 3.0]][b % 5] if b < 10 else rng.normal(size=2)
+        th[b] = h
+        hc = complex(h[0], h[1])
+        kinds = rng.integers(0, 6, S)
+        i1 = rng.integers(0, len(pts), S)
+        i2 = rng.integers(0, len(pts), S)
+        p1 = pts[i1, 0] + 1j * pts[i1, 1]
+        p2 = pts[i2, 0] + 1j * pts[i2, 1]
+        noise = rng.normal(size=S) + 1j * rng.normal(size=S)
+        z = np.select([kinds == 0, kinds == 1, kinds == 2, kinds == 3, kinds == 4],
+                      [p1 * hc, (p1 + p2) / 2 * hc, 0.0, p1 * hc + 1e-9 * noise, 30.0 * noise],
+                      p1 * hc + 0.3 * noise)
+        y[b, :, 0] = z.real
+        y[b, :, 1] = z.imag
+    return y, th
+
+
+@pytest.mark.parametrize("matrix,modem,snr", [
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", 2.0),
+    ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", 5.01),
+    ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", 6.77),
+    ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", 40.0),
+])
+def test_demap_and_metric_adversarial(data_dir, matrix, modem, snr):
+    """Bit-exact P0 (fast shared-reciprocal divisions with IEEE fallback) and
+    bit-exact hard metrics (single-precision screen with exact fallback) on
+    adversarial symbols, against the oracle demapper + parity count."""
+    ctx = ctx_for(data_dir, matrix, modem, False)
+    oc = oracle_for(data_dir, matrix, False)
+    om = O.Modem(os.path.join(data_dir, modem))
+    pts = om.points.reshape(-1, 2)
+    rng = np.random.default_rng(5)
+    B = 20
+    y, th = _adversarial_symbols(pts, ctx.S, B, rng)
+    var = 10.0 ** (-0.1 * snr)
+    ref = np.stack([om.demap(y[i], th[i], var) for i in range(B)])
+    got = ctx.demap(y, th, var)
+    assert np.array_equal(got, ref, equal_nan=True)
+    out = ctx.decode_frames(y, snr, true_h=th, histogram=True)
+    for i in range(B):
+        rr = (ref[i] > 0.5).astype(np.uint8)
+        assert out["metrics"][i][0] == abs(oc.parity_count(rr)), i
+
+
 @pytest.mark.parametrize("matrix,modem,snr,n", [
     ("PEG2304regular0.5.txt", "2bits_QPSK.txt", 2.0, 200),
     ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", 5.01, 100),
