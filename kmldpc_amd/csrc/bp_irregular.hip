@@ -10,10 +10,17 @@
 // Mapping (one workgroup of T threads per CU, persistent over codewords):
 //   * message slots (16 B per edge), the codeword's priors and the
 //     column->slot table (u16) in LDS;
-//   * thread t owns vn positions r*T + t and half-rows r*T + t; the planner
-//     sorts columns and rows by degree, so a wave almost always runs one
-//     degree, and every degree has its own fully unrolled instance (the chain
-//     states stay in registers);
+//   * the round plan (layout.hpp IrregularPlan) gives thread t its columns
+//     and half-rows in three rounds: in rounds 0 and 1 two items of one
+//     degree whose chains run interleaved (the second chain hides the first's
+//     fma / rcp latency; pairs up to degree kIrrVnPairMax / kIrrCnPairMax, the
+//     limit of the 168 registers of three waves per SIMD), in round 2 a single
+//     item; a wave runs one degree per round, every (degree, pairing) has its
+//     own fully unrolled instance (the chain states stay in registers), and
+//     the waves are placed so the 4 SIMDs get balanced VALU work.  Measured
+//     (BG2, 50 iterations, 16384 codewords): 25.0 ms with one item per round
+//     -> 21.25 ms; pair limits 5/8: 21.75, 5/10: 21.8, 7/8: 23.2 (pairs of
+//     degree 9 spill inside the loop);
 //   * check rows are split over lane pairs exactly like bp_regular.hip: the
 //     even lane runs the forward trellis, the odd lane the backward one, DPP
 //     swaps exchange the chain states, each lane finishes half of the row's
@@ -38,90 +45,120 @@ __device__ __forceinline__ double swap_pair(double x) {
 }
 __device__ __forceinline__ int swap_pair_i(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }
 
-// One column of degree D (binaryldpccodec.cc:177-213).
-template <int D, bool FAST>
-__device__ __forceinline__ void vn_column(double2 *slots, const unsigned short *cs, double p, unsigned char *hard) {
-  double c0s[D];
+// R columns of degree D (binaryldpccodec.cc:177-213), their chains
+// interleaved step by step so the dependent fma / rcp sequences overlap.
+template <int D, int R, bool FAST>
+__device__ __forceinline__ void vn_cols(double2 *slots, const unsigned short *const (&cs)[R], const double (&p)[R],
+                                        unsigned char *const (&hard)[R]) {
+  double c0s[R][D];
 #pragma unroll
-  for (int k = 0; k < D; ++k) c0s[k] = slots[cs[k]].x;
-  double a0 = p, a1 = 1.0 - p, al0[D], al1[D];
+  for (int r = 0; r < R; ++r)
 #pragma unroll
-  for (int k = 0; k < D; ++k) {
-    al0[k] = a0;
-    al1[k] = a1;
-    const double n0 = a0 * c0s[k];
-    const double n1 = a1 * (1.0 - c0s[k]);
-    if (k + 1 < D)
-      div2<FAST>(n0, n1, n0 + n1, a0, a1);
-    else
-      *hard = (unsigned char)hard_decision<FAST>(n0, n1);
+    for (int k = 0; k < D; ++k) c0s[r][k] = slots[cs[r][k]].x;
+  double a0[R], a1[R], al0[R][D], al1[R][D];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    a0[r] = p[r];
+    a1[r] = 1.0 - p[r];
   }
-  double b0 = 1.0, b1 = 1.0;
 #pragma unroll
-  for (int k = D - 1; k >= 0; --k) {
-    const bool unit = FAST && k == D - 1;  // beta = (1, 1)
-    const double t0 = unit ? al0[k] : al0[k] * b0;
-    const double t1 = unit ? al1[k] : al1[k] * b1;
-    double q0, q1;
-    div2<FAST>(t0, t1, t0 + t1, q0, q1);
-    slots[cs[k]] = make_double2(q0, q1);
-    if (k > 0) {
-      const double c0 = c0s[k];
-      if (unit) {  // (c0, 1 - c0) / (c0 + (1 - c0)): the sum rounds to exactly 1 (bp_common.hpp)
-        b0 = c0;
-        b1 = 1.0 - c0;
-      } else {
-        div2<FAST>(b0 * c0, b1 * (1.0 - c0), b0 * c0 + b1 * (1.0 - c0), b0, b1);
+  for (int k = 0; k < D; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      al0[r][k] = a0[r];
+      al1[r][k] = a1[r];
+      const double n0 = a0[r] * c0s[r][k];
+      const double n1 = a1[r] * (1.0 - c0s[r][k]);
+      if (k + 1 < D)
+        div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r]);
+      else
+        *hard[r] = (unsigned char)hard_decision<FAST>(n0, n1);
+    }
+  double b0[R], b1[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) b0[r] = b1[r] = 1.0;
+#pragma unroll
+  for (int k = D - 1; k >= 0; --k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool unit = FAST && k == D - 1;  // beta = (1, 1)
+      const double t0 = unit ? al0[r][k] : al0[r][k] * b0[r];
+      const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
+      double q0, q1;
+      div2<FAST>(t0, t1, t0 + t1, q0, q1);
+      slots[cs[r][k]] = make_double2(q0, q1);
+      if (k > 0) {
+        const double c0 = c0s[r][k];
+        if (unit) {  // (c0, 1 - c0) / (c0 + (1 - c0)): the sum rounds to exactly 1 (bp_common.hpp)
+          b0[r] = c0;
+          b1[r] = 1.0 - c0;
+        } else {
+          div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r]);
+        }
       }
     }
-  }
 }
 
-// Half of a check row of degree D (binaryldpccodec.cc:235-275), streamed step
-// by step; returns the forward state past the last edge (syndrom_soft) on the
-// even lane when SYN.
-template <int D, bool SYN, bool FAST>
-__device__ __forceinline__ double cn_half(double2 *slots, int base, int odd) {
+// Half of R check rows of degree D (binaryldpccodec.cc:235-275), streamed step
+// by step with the R rows interleaved; sv[r] = the forward state past the
+// last edge (syndrom_soft, read on the even lane) when SYN.
+template <int D, int R, bool SYN, bool FAST>
+__device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], int odd, double (&sv)[R]) {
   constexpr int S = (D + 1) / 2;  // states kept: x[0..S)
-  double x0[S], x1[S];
-  double s0 = 1.0, s1 = 0.0;
+  double x0[R][S], x1[R][S], s0[R], s1[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    s0[r] = 1.0;
+    s1[r] = 0.0;
+  }
 #pragma unroll
   for (int st = 0; st < D; ++st) {
     const bool advance = SYN || st + 1 < D;
-    double m0 = 0.0, m1 = 0.0;
+    double m0[R], m1[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      m0[r] = m1[r] = 0.0;
+      if (advance) {
+        const double2 m = slots[base[r] + (odd ? D - 1 - st : st)];
+        m0[r] = m.x;
+        m1[r] = m.y;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (st < S) {
+        x0[r][st] = s0[r];
+        x1[r][st] = s1[r];
+      }
+      if ((D & 1) && st == (D - 1) / 2) {  // middle edge: both states are current here
+        const double y0 = swap_pair(s0[r]), y1 = swap_pair(s1[r]);
+        const double t0 = s0[r] * y0 + s1[r] * y1;
+        const double t1 = s0[r] * y1 + s1[r] * y0;
+        const double q = clip_c2v<FAST>(div1<FAST>(t0, t0 + t1));
+        if (!odd) slots[base[r] + st].x = q;
+      }
+      if (st >= S) {
+        // c2v of edge (odd ? st : D-1-st) from (own state at D-1-st, partner state now)
+        const double y0 = swap_pair(s0[r]), y1 = swap_pair(s1[r]);
+        const double o0 = x0[r][D - 1 - st], o1 = x1[r][D - 1 - st];
+        const bool unit = FAST && st == D - 1;  // own state is the boundary (1, 0)
+        const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
+        const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
+        slots[base[r] + (odd ? st : D - 1 - st)].x = clip_c2v<FAST>(div1<FAST>(t0, t0 + t1));
+      }
+    }
     if (advance) {
-      const double2 m = slots[base + (odd ? D - 1 - st : st)];
-      m0 = m.x;
-      m1 = m.y;
-    }
-    if (st < S) {
-      x0[st] = s0;
-      x1[st] = s1;
-    }
-    if ((D & 1) && st == (D - 1) / 2) {  // middle edge: both states are current here
-      const double y0 = swap_pair(s0), y1 = swap_pair(s1);
-      const double t0 = s0 * y0 + s1 * y1;
-      const double t1 = s0 * y1 + s1 * y0;
-      const double q = clip_c2v<FAST>(div1<FAST>(t0, t0 + t1));
-      if (!odd) slots[base + st].x = q;
-    }
-    if (st >= S) {
-      // c2v of edge (odd ? st : D-1-st) from (own state at D-1-st, partner state now)
-      const double y0 = swap_pair(s0), y1 = swap_pair(s1);
-      const double o0 = x0[D - 1 - st], o1 = x1[D - 1 - st];
-      const bool unit = FAST && st == D - 1;  // own state is the boundary (1, 0)
-      const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
-      const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
-      slots[base + (odd ? st : D - 1 - st)].x = clip_c2v<FAST>(div1<FAST>(t0, t0 + t1));
-    }
-    if (advance) {
-      const bool unit = FAST && st == 0;
-      const double n0 = unit ? m0 : s0 * m0 + s1 * m1;
-      const double n1 = unit ? m1 : s0 * m1 + s1 * m0;
-      div2<FAST>(n0, n1, n0 + n1, s0, s1);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const bool unit = FAST && st == 0;
+        const double n0 = unit ? m0[r] : s0[r] * m0[r] + s1[r] * m1[r];
+        const double n1 = unit ? m1[r] : s0[r] * m1[r] + s1[r] * m0[r];
+        div2<FAST>(n0, n1, n0 + n1, s0[r], s1[r]);
+      }
     }
   }
-  return s0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) sv[r] = s0[r];
 }
 
 // falling wave priorities over a phase's rounds (see bp_regular.hip)
@@ -134,68 +171,84 @@ __device__ __forceinline__ void set_prio(int p) {
   }
 }
 
-template <bool FAST>
-__device__ __forceinline__ void vn_any(int d, double2 *slots, const unsigned short *cs, double p, unsigned char *h) {
+// Degree dispatch.  Paired (R = 2) instances exist up to the plan's pair
+// limits (kIrrVnPairMax / kIrrCnPairMax): the register budget of three waves
+// per SIMD holds two interleaved chains only up to those degrees.
+template <int D, int R, bool FAST>
+__device__ __forceinline__ void vn_cols_if(double2 *slots, const unsigned short *const (&cs)[R], const double (&p)[R],
+                                           unsigned char *const (&h)[R]) {
+  if constexpr (R == 1 || D <= kIrrVnPairMax) vn_cols<D, R, FAST>(slots, cs, p, h);
+}
+template <int R, bool FAST>
+__device__ __forceinline__ void vn_any(int d, double2 *slots, const unsigned short *const (&cs)[R], const double (&p)[R],
+                                       unsigned char *const (&h)[R]) {
   switch (d) {
-    case 1: vn_column<1, FAST>(slots, cs, p, h); break;
-    case 2: vn_column<2, FAST>(slots, cs, p, h); break;
-    case 3: vn_column<3, FAST>(slots, cs, p, h); break;
-    case 4: vn_column<4, FAST>(slots, cs, p, h); break;
-    case 5: vn_column<5, FAST>(slots, cs, p, h); break;
-    case 6: vn_column<6, FAST>(slots, cs, p, h); break;
-    case 7: vn_column<7, FAST>(slots, cs, p, h); break;
-    case 8: vn_column<8, FAST>(slots, cs, p, h); break;
-    default: vn_column<9, FAST>(slots, cs, p, h); break;
+    case 1: vn_cols_if<1, R, FAST>(slots, cs, p, h); break;
+    case 2: vn_cols_if<2, R, FAST>(slots, cs, p, h); break;
+    case 3: vn_cols_if<3, R, FAST>(slots, cs, p, h); break;
+    case 4: vn_cols_if<4, R, FAST>(slots, cs, p, h); break;
+    case 5: vn_cols_if<5, R, FAST>(slots, cs, p, h); break;
+    case 6: vn_cols_if<6, R, FAST>(slots, cs, p, h); break;
+    case 7: vn_cols_if<7, R, FAST>(slots, cs, p, h); break;
+    case 8: vn_cols_if<8, R, FAST>(slots, cs, p, h); break;
+    default: vn_cols_if<9, R, FAST>(slots, cs, p, h); break;
   }
 }
 
-template <bool SYN, bool FAST>
-__device__ __forceinline__ double cn_any(int d, double2 *slots, int base, int odd) {
+template <int D, int R, bool SYN, bool FAST>
+__device__ __forceinline__ void cn_halves_if(double2 *slots, const int (&base)[R], int odd, double (&sv)[R]) {
+  if constexpr (R == 1 || D <= kIrrCnPairMax) cn_halves<D, R, SYN, FAST>(slots, base, odd, sv);
+}
+template <int R, bool SYN, bool FAST>
+__device__ __forceinline__ void cn_any(int d, double2 *slots, const int (&base)[R], int odd, double (&sv)[R]) {
   switch (d) {
-    case 2: return cn_half<2, SYN, FAST>(slots, base, odd);
-    case 3: return cn_half<3, SYN, FAST>(slots, base, odd);
-    case 4: return cn_half<4, SYN, FAST>(slots, base, odd);
-    case 5: return cn_half<5, SYN, FAST>(slots, base, odd);
-    case 6: return cn_half<6, SYN, FAST>(slots, base, odd);
-    case 7: return cn_half<7, SYN, FAST>(slots, base, odd);
-    case 8: return cn_half<8, SYN, FAST>(slots, base, odd);
-    case 9: return cn_half<9, SYN, FAST>(slots, base, odd);
-    default: return cn_half<10, SYN, FAST>(slots, base, odd);
+    case 2: cn_halves_if<2, R, SYN, FAST>(slots, base, odd, sv); break;
+    case 3: cn_halves_if<3, R, SYN, FAST>(slots, base, odd, sv); break;
+    case 4: cn_halves_if<4, R, SYN, FAST>(slots, base, odd, sv); break;
+    case 5: cn_halves_if<5, R, SYN, FAST>(slots, base, odd, sv); break;
+    case 6: cn_halves_if<6, R, SYN, FAST>(slots, base, odd, sv); break;
+    case 7: cn_halves_if<7, R, SYN, FAST>(slots, base, odd, sv); break;
+    case 8: cn_halves_if<8, R, SYN, FAST>(slots, base, odd, sv); break;
+    case 9: cn_halves_if<9, R, SYN, FAST>(slots, base, odd, sv); break;
+    default: cn_halves_if<10, R, SYN, FAST>(slots, base, odd, sv); break;
   }
 }
 
-template <int T, int RV, int RC, bool SYN, bool FAST>
+// Column / row of the lane in round r of the plan (layout.hpp IrregularPlan):
+// rounds 0 and 1 pair two items of one degree, round 2 holds single items.
+template <int T, bool SYN, bool FAST>
 __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, int cw, double2 *slots,
                                            const unsigned short *cslot, const double *p0s, unsigned char *cch, int odd,
-                                           int &iter_out, bool &conv_out) {
-  const int tid = threadIdx.x;
+                                           const int (&vcol)[3], const int (&crow)[3], int &iter_out, bool &conv_out) {
   int iter = 0;
   bool conv = false;
+  auto prior = [&](int v) { return v >= c.punct ? p0s[v - c.punct] : 0.5; };  // :126-134
   for (; iter < a.iter_count; ++iter) {
-    // VN rounds: per-round column data from the (cached) planner arrays and
-    // the LDS priors, so nothing is indexed by round in registers
-#pragma unroll 1
-    for (int r = 0; r < RV; ++r) {
-      set_prio(3 - r);
-      const int pos = r * T + tid;
-      if (pos < c.N) {
-        const int v = c.vn_order[pos];
-        const int b = c.col_ptr[v];
-        const double pr = v >= c.punct ? p0s[v - c.punct] : 0.5;  // :126-134
-        vn_any<FAST>(c.col_ptr[v + 1] - b, slots, cslot + b, pr, &cch[v]);
-      }
+    set_prio(3);
+    if (vcol[0] >= 0) {  // paired round: two columns of one degree, interleaved
+      const int b0 = c.col_ptr[vcol[0]], b1 = c.col_ptr[vcol[1]];
+      const unsigned short *const cs[2] = {cslot + b0, cslot + b1};
+      const double p[2] = {prior(vcol[0]), prior(vcol[1])};
+      unsigned char *const h[2] = {&cch[vcol[0]], &cch[vcol[1]]};
+      vn_any<2, FAST>(c.col_ptr[vcol[0] + 1] - b0, slots, cs, p, h);
+    }
+    set_prio(1);
+    if (vcol[2] >= 0) {
+      const int b = c.col_ptr[vcol[2]];
+      const unsigned short *const cs[1] = {cslot + b};
+      const double p[1] = {prior(vcol[2])};
+      unsigned char *const h[1] = {&cch[vcol[2]]};
+      vn_any<1, FAST>(c.col_ptr[vcol[2] + 1] - b, slots, cs, p, h);
     }
     __syncthreads();
 
     int fail = 0;
 #pragma unroll 1
-    for (int r = 0; r < RC; ++r) {
-      const int q = (r * T + tid) >> 1;
+    for (int r = 0; r < 3; ++r) {
       int p = 0, d = 0;
-      if (q < c.M) {
-        const int row = c.cn_order[q];
-        const int base = c.row_ptr[row];
-        d = c.row_ptr[row + 1] - base;
+      if (crow[r] >= 0) {
+        const int base = c.row_ptr[crow[r]];
+        d = c.row_ptr[crow[r] + 1] - base;
         const int lo = odd ? (d + 1) / 2 : 0, hi = odd ? d : (d + 1) / 2;
         for (int k = lo; k < hi; ++k) p ^= cch[c.row_col[base + k]];
       }
@@ -205,17 +258,21 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
     // the OR over the workgroup is folded into the CN phase's closing barrier
     // (speculative CN, as in bp_regular.hip); syndromes are kept until the
     // phase is known to count
-    double sv[RC];
-#pragma unroll
-    for (int r = 0; r < RC; ++r) {
-      set_prio(2 - r);
-      const int q = (r * T + tid) >> 1;
-      sv[r] = 0.0;
-      if (q < c.M) {  // both lanes of a pair agree
-        const int row = c.cn_order[q];
-        const int base = c.row_ptr[row];
-        sv[r] = cn_any<SYN, FAST>(c.row_ptr[row + 1] - base, slots, base, odd);
-      }
+    double sv[3] = {0.0, 0.0, 0.0};
+    set_prio(2);
+    if (crow[0] >= 0) {  // both lanes of a pair agree
+      const int base[2] = {c.row_ptr[crow[0]], c.row_ptr[crow[1]]};
+      double s2[2];
+      cn_any<2, SYN, FAST>(c.row_ptr[crow[0] + 1] - base[0], slots, base, odd, s2);
+      sv[0] = s2[0];
+      sv[1] = s2[1];
+    }
+    set_prio(0);
+    if (crow[2] >= 0) {
+      const int base[1] = {c.row_ptr[crow[2]]};
+      double s1[1];
+      cn_any<1, SYN, FAST>(c.row_ptr[crow[2] + 1] - base[0], slots, base, odd, s1);
+      sv[2] = s1[0];
     }
     if (!__syncthreads_or(fail)) {
       conv = true;
@@ -223,17 +280,15 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
     }
     if constexpr (SYN) {
 #pragma unroll
-      for (int r = 0; r < RC; ++r) {
-        const int q = (r * T + tid) >> 1;
-        if (q < c.M && !odd) a.syn[(long long)cw * c.M + c.cn_order[q]] = sv[r];  // alpha past the last edge (:274)
-      }
+      for (int r = 0; r < 3; ++r)
+        if (crow[r] >= 0 && !odd) a.syn[(long long)cw * c.M + crow[r]] = sv[r];  // alpha past the last edge (:274)
     }
   }
   iter_out = iter;
   conv_out = conv;
 }
 
-template <int T, int RV, int RC, bool SYN>
+template <int T, bool SYN>
 __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, unsigned int *queue, int fast_allowed) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
@@ -245,6 +300,12 @@ __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, 
   unsigned char *cch = smem + (size_t)c.E * 18 + (size_t)c.cc_len * 8 + kRedBytes;
 
   for (int e = tid; e < c.E; e += T) cslot[e] = (unsigned short)c.col_slot[e];
+  int vcol[3], crow[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    vcol[r] = c.irr_vn[r * T + tid];
+    crow[r] = c.irr_cn[r * (T / 2) + (tid >> 1)];
+  }
 
   for (;;) {
     __syncthreads();
@@ -272,9 +333,9 @@ __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, 
     int iter = 0;
     bool conv = false;
     if (fast)
-      decode_irr<T, RV, RC, SYN, true>(c, a, cw, slots, cslot, p0s, cch, odd, iter, conv);
+      decode_irr<T, SYN, true>(c, a, cw, slots, cslot, p0s, cch, odd, vcol, crow, iter, conv);
     else
-      decode_irr<T, RV, RC, SYN, false>(c, a, cw, slots, cslot, p0s, cch, odd, iter, conv);
+      decode_irr<T, SYN, false>(c, a, cw, slots, cslot, p0s, cch, odd, vcol, crow, iter, conv);
 
     if (a.iter_count > 0) {
       if (a.uu_hat) {
@@ -330,9 +391,9 @@ __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, 
   }
 }
 
-template <int T, int RV, int RC, bool SYN>
+template <int T, bool SYN>
 hipError_t launch_irr_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
-  auto kern = bp_irregular_kernel<T, RV, RC, SYN>;
+  auto kern = bp_irregular_kernel<T, SYN>;
   const size_t lds = (size_t)c.E * 18 + (size_t)c.cc_len * 8 + kRedBytes + (size_t)c.N;
   hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -350,11 +411,11 @@ hipError_t launch_irr_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int 
 }  // namespace
 
 hipError_t launch_bp_irregular(const DevCode &c, const BpLaunch &a, hipStream_t s) {
-  constexpr int T = 768, RV = 3, RC = 3;
+  constexpr int T = kIrrThreads;
   if ((long long)c.E * 18 + 8LL * c.cc_len + kRedBytes + c.N > 160 * 1024 || c.E > 65535) return hipErrorNotSupported;
-  if (!c.irr_ok || c.N > RV * T || 2 * c.M > RC * T) return hipErrorNotSupported;
+  if (!c.irr_ok || !c.irr_vn) return hipErrorNotSupported;
   const int fast = c.dv_max <= kFastMaxColumnDegree ? 1 : 0;
-  return a.syn ? launch_irr_t<T, RV, RC, true>(c, a, s, fast) : launch_irr_t<T, RV, RC, false>(c, a, s, fast);
+  return a.syn ? launch_irr_t<T, true>(c, a, s, fast) : launch_irr_t<T, false>(c, a, s, fast);
 }
 
 }  // namespace kml

@@ -50,7 +50,7 @@ __device__ __forceinline__ void stage_exp_table(uint64_t *dst) {  // dst: a __sh
 // that domain; callers fall back to kml_exp outside it.
 __device__ __forceinline__ bool exp_core_ok(double x) {
   const double a = fabs(x);  // branch-free: (2^-54 <= |x| < 512) or x == 0
-  return (a >= 0x1p-54) & (a < 512.0) | (x == 0.0);
+  return ((a >= 0x1p-54) & (a < 512.0)) | (x == 0.0);
 }
 __device__ __forceinline__ double exp_core(double x, lds_exptab tab) {
   const double InvLn2N = 0x1.71547652b82fep0 * 128;

@@ -23,6 +23,8 @@ struct DevCode {
   int M, N, E, K, cc_len, punct, info_off, chk, Kw, dv_max, dc_max, is5g, active;
   int regular;  // every column has degree dv_max and every row dc_max
   int irr_ok;   // column degrees in [1, 9] and row degrees in [2, 10] (bp_irregular.hip)
+  // Round plan of bp_irregular.hip (layout.hpp IrregularPlan); null when none fits.
+  const int32_t *irr_vn, *irr_cn;
   // LDS placement plan of bp_regular.hip (layout.hpp); null when the code does
   // not take that kernel.  vn_order then holds the planned column order.
   const int32_t *reg_c2v;  // aligned with col_slot: byte offset of the c2v message
@@ -75,6 +77,9 @@ struct BpLaunch {
 };
 
 hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s);
+constexpr int kIrrThreads = 768;  // threads per workgroup of bp_irregular.hip (its plan is made for this)
+constexpr int kIrrVnPairMax = 4;  // highest column degree bp_irregular.hip pairs
+constexpr int kIrrCnPairMax = 8;  // highest row degree it pairs
 hipError_t launch_bp_irregular(const DevCode &c, const BpLaunch &a, hipStream_t s);
 // Cooperative kernel for regular codes whose slots exceed the LDS: groups of
 // workgroups on one XCD share a codeword.  0 groups = not applicable.

@@ -350,3 +350,116 @@ bool plan_partition(const LdpcCode &L, int G, PartitionPlan &out) {
 }
 
 }  // namespace kml
+
+namespace kml {
+
+namespace {
+
+// One wave's worth of items (64 columns, or 32 rows) for one round.
+struct WaveItems {
+  std::vector<int32_t> a, b;  // a: the (first) items; b: the second items of a pair wave
+  double cost = 0;
+};
+
+// items[d] = the items of degree d.  cost(d) models one item's VALU work.
+// Returns false when the items do not fit W pair waves + W single waves.
+bool plan_rounds(std::vector<std::vector<int32_t>> items, int per_wave, int W, int pair_max, double (*cost)(int),
+                 std::vector<WaveItems> &pairs, std::vector<WaveItems> &singles) {
+  const int dmax = (int)items.size() - 1;
+  pairs.clear();
+  singles.clear();
+  // pair waves from the highest degrees (up to pair_max): 2 * per_wave items of one degree
+  for (int d = std::min(dmax, pair_max); d >= 0 && (int)pairs.size() < W; --d)
+    while ((int)items[d].size() >= 2 * per_wave && (int)pairs.size() < W) {
+      WaveItems w;
+      w.a.assign(items[d].begin(), items[d].begin() + per_wave);
+      w.b.assign(items[d].begin() + per_wave, items[d].begin() + 2 * per_wave);
+      items[d].erase(items[d].begin(), items[d].begin() + 2 * per_wave);
+      w.cost = 2 * per_wave * cost(d);
+      pairs.push_back(std::move(w));
+    }
+  // the rest as single waves, highest degree first; a partial wave is topped up
+  // with the next degree's items (a mixed wave)
+  WaveItems cur;
+  for (int d = dmax; d >= 0; --d)
+    for (int32_t it : items[d]) {
+      cur.a.push_back(it);
+      cur.cost += cost(d);
+      if ((int)cur.a.size() == per_wave) {
+        singles.push_back(std::move(cur));
+        cur = WaveItems();
+      }
+    }
+  if (!cur.a.empty()) singles.push_back(std::move(cur));
+  return (int)singles.size() <= W;
+}
+
+// Place pair waves and single waves on lane waves 0..W-1 so that the SIMD
+// totals (wave w on SIMD w % 4) are balanced: longest-processing-time first,
+// each SIMD taking W/4 pair waves and W/4 single waves.
+void place_waves(const std::vector<WaveItems> &pairs, const std::vector<WaveItems> &singles, int W,
+                 std::vector<int> &pair_of, std::vector<int> &single_of) {
+  const int per = W / 4;
+  std::vector<double> load(4, 0.0);
+  std::vector<std::vector<int>> simd_waves(4);
+  for (int w = 0; w < W; ++w) simd_waves[w % 4].push_back(w);
+  pair_of.assign(W, -1);
+  single_of.assign(W, -1);
+  auto lpt = [&](const std::vector<WaveItems> &v, std::vector<int> &of) {
+    std::vector<int> idx(v.size());
+    for (size_t i = 0; i < v.size(); ++i) idx[i] = (int)i;
+    std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return v[x].cost > v[y].cost; });
+    std::vector<int> used(4, 0);
+    for (int i : idx) {
+      int best = -1;
+      for (int s = 0; s < 4; ++s)
+        if (used[s] < per && (best < 0 || load[s] < load[best])) best = s;
+      of[simd_waves[best][used[best]++]] = i;
+      load[best] += v[i].cost;
+    }
+  };
+  lpt(pairs, pair_of);
+  lpt(singles, single_of);
+}
+
+double vn_cost(int d) { return 3.0 * d - 1.0; }  // div2 steps of a column (forward d-1, backward 2d-1)
+double cn_cost(int d) { return 1.5 * d; }        // per half-row: advances + half the c2v outputs
+
+}  // namespace
+
+bool plan_irregular(const LdpcCode &L, int T, int vn_pair_max, int cn_pair_max, IrregularPlan &out) {
+  if (T % 256) return false;
+  const int W = T / 64;
+  std::vector<std::vector<int32_t>> cols(L.dv_max + 1), rows(L.dc_max + 1);
+  for (int32_t v : L.vn_order) cols[L.col_ptr[v + 1] - L.col_ptr[v]].push_back(v);
+  for (int32_t r : L.cn_order) rows[L.row_ptr[r + 1] - L.row_ptr[r]].push_back(r);
+  std::vector<WaveItems> vp, vs, cp, cs;
+  if (!plan_rounds(cols, 64, W, vn_pair_max, vn_cost, vp, vs) ||
+      !plan_rounds(rows, 32, W, cn_pair_max, cn_cost, cp, cs))
+    return false;
+  std::vector<int> vp_of, vs_of, cp_of, cs_of;
+  place_waves(vp, vs, W, vp_of, vs_of);
+  place_waves(cp, cs, W, cp_of, cs_of);
+  out.vn.assign(3 * T, -1);
+  out.cn.assign(3 * T / 2, -1);
+  for (int w = 0; w < W; ++w) {
+    if (vp_of[w] >= 0)
+      for (int l = 0; l < 64; ++l) {
+        out.vn[w * 64 + l] = vp[vp_of[w]].a[l];
+        out.vn[T + w * 64 + l] = vp[vp_of[w]].b[l];
+      }
+    if (vs_of[w] >= 0)
+      for (size_t l = 0; l < vs[vs_of[w]].a.size(); ++l) out.vn[2 * T + w * 64 + l] = vs[vs_of[w]].a[l];
+    if (cp_of[w] >= 0)
+      for (int l = 0; l < 32; ++l) {
+        out.cn[w * 32 + l] = cp[cp_of[w]].a[l];
+        out.cn[T / 2 + w * 32 + l] = cp[cp_of[w]].b[l];
+      }
+    if (cs_of[w] >= 0)
+      for (size_t l = 0; l < cs[cs_of[w]].a.size(); ++l) out.cn[T + w * 32 + l] = cs[cs_of[w]].a[l];
+  }
+  return true;
+}
+
+}  // namespace kml
+

@@ -68,3 +68,26 @@ struct PartitionPlan {
 bool plan_partition(const LdpcCode &L, int G, PartitionPlan &out);
 
 }  // namespace kml
+
+namespace kml {
+
+// Round plan of the irregular-code BP kernel (bp_irregular.hip): T threads in
+// W = T/64 waves, three rounds per phase.  In rounds 0 and 1 a lane owns TWO
+// columns (two half-rows) of the same degree and runs their chains
+// interleaved; round 2 holds single columns (half-rows).  Every wave of a
+// round runs one degree (64 columns, or 32 rows as lane pairs), except at
+// most a few waves that mix the leftovers of two degrees.  Pairs are formed
+// from the highest degrees up to a limit (the longest dependent chains gain
+// most from a second chain; the limits keep two chains within the registers), and the waves are placed so that the modelled VALU work of
+// the 4 SIMDs (wave w runs on SIMD w % 4) is balanced.  Any placement gives
+// the same decoder output: it only moves work between lanes.
+struct IrregularPlan {
+  std::vector<int32_t> vn;  // [3*T]: column of position r*T + t, -1 = idle
+  std::vector<int32_t> cn;  // [3*T/2]: row of lane pair r*T/2 + (t >> 1), -1 = idle
+};
+
+// False when the code's degree groups do not fit three rounds of T lanes.
+bool plan_irregular(const LdpcCode &L, int T, int vn_pair_max, int cn_pair_max, IrregularPlan &out);
+
+}  // namespace kml
+
