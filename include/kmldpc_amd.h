@@ -233,7 +233,9 @@ int kml_math_probe(kml_ctx *ctx, const double *in, int n, double *out);
 /* Device-side probe of the soft metric's log (kml_log, glibc-exact): out[i] = log(in[i]). */
 int kml_log_probe(kml_ctx *ctx, const double *in, int n, double *out);
 /* Device-side probe of the decoder's shared-reciprocal division: in[n][3] =
- * (n0, n1, s) -> out[n][4] = (fast n0/s, fast n1/s, IEEE n0/s, IEEE n1/s). */
+ * (n0, n1, s) -> out[n][8] = (fast n0/s, fast n1/s, IEEE n0/s, IEEE n1/s,
+ * CN-phase n0/s, CN-phase n1/s (near-one reciprocal), the near-one reciprocal
+ * formula of s, hipcc's refined reciprocal of s) — see bp_common.hpp. */
 int kml_div_probe(kml_ctx *ctx, const double *in, int n, double *out);
 
 #ifdef __cplusplus

@@ -337,7 +337,7 @@ class Context:
 
     def div_probe(self, x):
         x = _f64(x).reshape(-1, 3)
-        out = np.zeros((x.shape[0], 4))
+        out = np.zeros((x.shape[0], 8))
         self._chk(lib().kml_div_probe(self._h, _p(x), x.shape[0], _p(out)), "kml_div_probe")
         return out
 

@@ -38,18 +38,70 @@ __device__ __forceinline__ void lds_st(unsigned a, T v) {
 // path only for codewords whose priors are 0, 1 or in [2^-40, 1-2^-40] on codes
 // with column degree <= 20, which bounds every nonzero message, sum and quotient
 // of the decoder below 1 and above 2^-840 ("Exact fast division").
-template <bool FAST>
+// hipcc's reciprocal refinement of an f64 '/': v_rcp_f64 and two Newton steps.
+__device__ __forceinline__ double rcp_refine(double s) {
+  const double ns = -s;
+  double r = __builtin_amdgcn_rcp(s);
+  double e = fma(ns, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(ns, r, 1.0);
+  return fma(r, e, r);
+}
+
+// The reciprocal of a sum within 2^-40 of 1, correctly rounded.  Every
+// normalisation sum of the CN phase is one (s = (s0 + s1)(m0 + m1) of two
+// normalised pairs, within a few ulps of 1).  With u = 1 - s (exact),
+// 1/s = 1 + u + u^2 + ..., which rounds to 1 + u, except that when 1 + u is a
+// midpoint (s < 1 an odd multiple of 2^-53 below 1) the positive u^2 term
+// rounds it up; 1 + (u + 2^-80) reproduces both (u + 2^-80 is exact, and
+// 2^-80 breaks exactly the ties u^2 breaks).  So rcp_near1(s) = RN(1/s): three
+// adds instead of a quarter-rate v_rcp_f64 and four fmas.  With a correctly
+// rounded reciprocal the division tail (m = RN(n r), q = fma(fma(-s, m, n), r,
+// m)) is off only when n / s lies within 2^-51 ulp of a rounding midpoint;
+// tools/verify_cn_division.py enumerates every such n for |s - 1| <= 64 ulp
+// and evaluates the tail exactly: it always rounds to RN(n / s).  hipcc's
+// refinement is NOT RN(1/s) on six of these s (s = 1 - k 2^-53, k = 3, 5, ...,
+// 13: one ulp low), and hipcc's '/' then misrounds three significands (the
+// GPU test test_cn_reciprocal_exhaustive shows both).
+constexpr double kNearOne = 0x1p-40;
+__device__ __forceinline__ double rcp_near1(double s) { return 1.0 + ((1.0 - s) + 0x1p-80); }
+__device__ __forceinline__ double rcp_cn(double s) {
+  double r = rcp_near1(s);
+  if (__builtin_expect(!(fabs(1.0 - s) <= kNearOne), 0)) r = rcp_refine(s);  // never seen in a CN phase
+  return r;
+}
+
+// Reciprocals of the R sums of one CN step (R independent rows): the near-one
+// formula, or — when any sum of the lane is out of its range (not seen in a
+// CN phase) — hipcc's refinement for all R, as the other FAST divisions use.
+// One branch per step keeps the R rows' chains in one scheduling region.
+template <int R>
+__device__ __forceinline__ void rcp_cn_rows(const double (&s)[R], double (&r)[R]) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    r[i] = rcp_near1(s[i]);
+    ok = ok & (fabs(1.0 - s[i]) <= kNearOne);
+  }
+  if (__builtin_expect(!ok, 0)) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) r[i] = rcp_refine(s[i]);
+  }
+}
+// n / s from a reciprocal r of s that is exact for it (FAST division tail).
+__device__ __forceinline__ double qdiv_r(double n, double s, double r) {
+  const double m = n * r;
+  return fma(fma(-s, m, n), r, m);
+}
+
+template <bool FAST, bool CN = false>
 __device__ __forceinline__ void div2(double n0, double n1, double s, double &q0, double &q1) {
   if constexpr (!FAST) {
     q0 = n0 / s;
     q1 = n1 / s;
   } else {
     const double ns = -s;
-    double r = __builtin_amdgcn_rcp(s);
-    double e = fma(ns, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(ns, r, 1.0);
-    r = fma(r, e, r);
+    const double r = CN ? rcp_cn(s) : rcp_refine(s);
     const double m0 = n0 * r;
     const double m1 = n1 * r;
     const double f0 = fma(ns, m0, n0);
@@ -59,17 +111,13 @@ __device__ __forceinline__ void div2(double n0, double n1, double s, double &q0,
   }
 }
 
-template <bool FAST>
+template <bool FAST, bool CN = false>
 __device__ __forceinline__ double div1(double n0, double s) {
   if constexpr (!FAST) {
     return n0 / s;
   } else {
     const double ns = -s;
-    double r = __builtin_amdgcn_rcp(s);
-    double e = fma(ns, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(ns, r, 1.0);
-    r = fma(r, e, r);
+    const double r = CN ? rcp_cn(s) : rcp_refine(s);
     const double m0 = n0 * r;
     const double f0 = fma(ns, m0, n0);
     return fma(f0, r, m0);

@@ -265,7 +265,7 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
             const bool unit = FAST && st == DC - 1;
             const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
             const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
-            q[r] = clip_c2v<FAST>(div1<FAST>(t0, t0 + t1));
+            q[r] = clip_c2v<FAST>(div1<FAST, true>(t0, t0 + t1));
           }
         }
         if (advance) {
@@ -274,7 +274,7 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
             const bool unit = FAST && st == 0;
             const double n0 = unit ? m0[r] : s0[r] * m0[r] + s1[r] * m1[r];
             const double n1 = unit ? m1[r] : s0[r] * m1[r] + s1[r] * m0[r];
-            div2<FAST>(n0, n1, n0 + n1, s0[r], s1[r]);
+            div2<FAST, true>(n0, n1, n0 + n1, s0[r], s1[r]);
           }
         }
         if (st >= H) {
@@ -718,7 +718,7 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
             const bool unit = FAST && st == DC - 1;
             const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
             const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
-            const double q = clip_c2v<FAST>(div1<FAST>(t0, t0 + t1));
+            const double q = clip_c2v<FAST>(div1<FAST, true>(t0, t0 + t1));
             if (cact[r]) *reinterpret_cast<double *>(smem + cbase[r] + (odd ? st : DC - 1 - st) * 16) = q;
           }
         }
@@ -728,7 +728,7 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
             const bool unit = FAST && st == 0;
             const double n0 = unit ? m0[r] : s0[r] * m0[r] + s1[r] * m1[r];
             const double n1 = unit ? m1[r] : s0[r] * m1[r] + s1[r] * m0[r];
-            div2<FAST>(n0, n1, n0 + n1, s0[r], s1[r]);
+            div2<FAST, true>(n0, n1, n0 + n1, s0[r], s1[r]);
           }
         }
       }

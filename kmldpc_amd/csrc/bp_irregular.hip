@@ -134,7 +134,7 @@ __device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], 
         const double y0 = swap_pair(s0[r]), y1 = swap_pair(s1[r]);
         const double t0 = s0[r] * y0 + s1[r] * y1;
         const double t1 = s0[r] * y1 + s1[r] * y0;
-        const double q = clip_c2v<FAST>(div1<FAST>(t0, t0 + t1));
+        const double q = clip_c2v<FAST>(div1<FAST, true>(t0, t0 + t1));
         if (!odd) slots[base[r] + st].x = q;
       }
       if (st >= S) {
@@ -144,7 +144,7 @@ __device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], 
         const bool unit = FAST && st == D - 1;  // own state is the boundary (1, 0)
         const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
         const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
-        slots[base[r] + (odd ? st : D - 1 - st)].x = clip_c2v<FAST>(div1<FAST>(t0, t0 + t1));
+        slots[base[r] + (odd ? st : D - 1 - st)].x = clip_c2v<FAST>(div1<FAST, true>(t0, t0 + t1));
       }
     }
     if (advance) {
@@ -153,7 +153,7 @@ __device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], 
         const bool unit = FAST && st == 0;
         const double n0 = unit ? m0[r] : s0[r] * m0[r] + s1[r] * m1[r];
         const double n1 = unit ? m1[r] : s0[r] * m1[r] + s1[r] * m0[r];
-        div2<FAST>(n0, n1, n0 + n1, s0[r], s1[r]);
+        div2<FAST, true>(n0, n1, n0 + n1, s0[r], s1[r]);
       }
     }
   }

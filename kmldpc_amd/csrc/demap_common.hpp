@@ -17,17 +17,9 @@ __device__ __forceinline__ double prob_clip(double v) {  // utility.cc:18-26
   return v;
 }
 
-// Quotient n / s from a refined reciprocal r of s: div2's FAST sequence
+// Quotient n / s from a refined reciprocal r of s (rcp_refine): div2's FAST sequence
 // (bp_common.hpp), bit-identical to an IEEE division when s is normal, n is 0
 // or at least 2^-969, the quotient is normal and the exponent gap is below 768.
-__device__ __forceinline__ double rcp_refine(double s) {
-  const double ns = -s;
-  double r = __builtin_amdgcn_rcp(s);
-  double e = fma(ns, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(ns, r, 1.0);
-  return fma(r, e, r);
-}
 __device__ __forceinline__ double qdiv(double n, double s, double r) {
   const double m = n * r;
   return fma(fma(-s, m, n), r, m);

@@ -514,13 +514,19 @@ __global__ void div_probe_kernel(const double *in, int n, double *out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double n0 = in[3 * i], n1 = in[3 * i + 1], s = in[3 * i + 2];
-  double q0, q1, r0, r1;
+  double q0, q1, r0, r1, c0, c1;
   div2<true>(n0, n1, s, q0, q1);
   div2<false>(n0, n1, s, r0, r1);
-  out[4 * i] = q0;
-  out[4 * i + 1] = q1;
-  out[4 * i + 2] = r0;
-  out[4 * i + 3] = r1;
+  div2<true, true>(n0, n1, s, c0, c1);
+  double *o = out + 8 * (long long)i;
+  o[0] = q0;
+  o[1] = q1;
+  o[2] = r0;
+  o[3] = r1;
+  o[4] = c0;
+  o[5] = c1;
+  o[6] = rcp_near1(s);
+  o[7] = rcp_refine(s);
 }
 }  // namespace
 

@@ -129,6 +129,73 @@ def test_fast_division_is_ieee_exact(data_dir):
         assert np.array_equal(out[:, 1], out[:, 3]), scale_exp
 
 
+def _near_midpoint_significands(K, width):
+    """Significands N in [2^52, 2^53) with (K N) mod 2^53 within width + 8 below
+    / 8 above 2^52, and N near the ends of the binade: the only n for which
+    n / s, s = 1 - K 2^-53, can be rounded wrongly by the CN division's last
+    fma (tools/verify_cn_division.py derives and checks this exactly)."""
+    two52, two53 = 2 ** 52, 2 ** 53
+    out = set(range(two53 - 256, two53)) | set(range(two52, two52 + 256))
+    t = 0
+    while K % 2 == 0:
+        K //= 2
+        t += 1
+    mod = two53 >> t
+    inv = pow(K % mod, -1, mod)
+    for B in range(two52 - width - 8, two52 + 9):
+        if B % (1 << t) == 0:
+            n0 = (inv * (B >> t)) % mod
+            out.update(n for n in (n0 + i * mod for i in range(1 << t)) if two52 <= n < two53)
+    return sorted(out)
+
+
+def test_cn_reciprocal_exhaustive(data_dir):
+    """The CN phases' near-one reciprocal (bp_common.hpp rcp_near1) is RN(1/s)
+    on every double s with |s - 1| <= 2^-40 (1 + j 2^-52, j <= 2^12, and
+    1 - k 2^-53, k <= 2^13).  hipcc's refined reciprocal is not (one ulp low on
+    s = 1 - k 2^-53, k = 3, 5, ..., 13), and its '/' then misrounds a few n / s:
+    on every near-midpoint candidate n the CN division equals IEEE division
+    and '/' is reported; random normalisation-like pairs and sums far from 1
+    (the fallback) are checked too."""
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    j = np.arange(0, 2 ** 12 + 1, dtype=np.float64)
+    k = np.arange(1, 2 ** 13 + 1, dtype=np.float64)
+    s = np.concatenate([1.0 + j * 2.0 ** -52, 1.0 - k * 2.0 ** -53])
+    assert s.size == 12289 and np.all(np.abs(s - 1.0) <= 2.0 ** -40)
+    rng = np.random.default_rng(3)
+    n0 = rng.random(s.size) * s
+    x = np.stack([n0, s - n0, s], axis=1)
+    out = ctx.div_probe(x)
+    assert np.array_equal(out[:, 6], 1.0 / s)  # near-one formula == RN(1/s) for every s
+    print(f"hipcc's refinement != RN(1/s) on {int(np.sum(out[:, 7] != 1.0 / s))} of {s.size} s")
+    assert np.array_equal(out[:, 4], x[:, 0] / x[:, 2]) and np.array_equal(out[:, 5], x[:, 1] / x[:, 2])
+    # near-midpoint candidates: s = 1 - K 2^-53 for K in [-32, 16] (K = -2j: s = 1 + j 2^-52)
+    rows = []
+    for K in [kk for kk in range(-32, 17) if kk and (kk > 0 or kk % 2 == 0)]:
+        sv = 1.0 - K * 2.0 ** -53
+        for N in _near_midpoint_significands(K, K * K):
+            rows.append((N * 2.0 ** -53, sv))
+    x = np.array([(n, 0.0, sv) for n, sv in rows])
+    out = ctx.div_probe(x)
+    ref = x[:, 0] / x[:, 2]
+    assert np.array_equal(out[:, 4], ref)
+    print(f"near-midpoint candidates: {len(rows)}; hipcc '/' misrounds {int(np.sum(out[:, 2] != ref))}")
+    # random normalisation-like pairs (products of normalised pairs) and sums far from 1
+    n = 400000
+    a = rng.random(n)
+    b = rng.random(n)
+    a0, a1 = a / (a + (1 - a)), (1 - a) / (a + (1 - a))
+    b0, b1 = b / (b + (1 - b)), (1 - b) / (b + (1 - b))
+    m0 = a0 * b0 + a1 * b1
+    m1 = a0 * b1 + a1 * b0
+    far0 = rng.random(n) * 2.0 ** -rng.uniform(0, 40, n)
+    far1 = rng.random(n) * 2.0 ** -rng.uniform(0, 40, n)
+    for p0, p1 in ((m0, m1), (far0, far1)):
+        x = np.stack([p0, p1, p0 + p1], axis=1)
+        out = ctx.div_probe(x)
+        assert np.array_equal(out[:, 4], x[:, 0] / x[:, 2]) and np.array_equal(out[:, 5], x[:, 1] / x[:, 2])
+
+
 @pytest.mark.parametrize("case", CASES)
 def test_bp_golden_vectors(case, data_dir):
     """Decode the reference's own P0 vectors: every output bit-exact."""
