@@ -94,6 +94,15 @@ __device__ __forceinline__ double qdiv_r(double n, double s, double r) {
   return fma(fma(-s, m, n), r, m);
 }
 
+// One CN step's normalisations for R rows: the c2v quotients clip(t0 / ts)
+// and the chain states (n0, n1) / (n0 + n1) (binaryldpccodec.cc:241-266), the
+// sums' reciprocals from rcp_cn_rows on the FAST path, IEEE divisions else.
+template <int R, bool FAST>
+__device__ __forceinline__ void cn_c2v_rows(const double (&t0)[R], const double (&ts)[R], double (&q)[R]);
+template <int R, bool FAST>
+__device__ __forceinline__ void cn_norm_rows(const double (&n0)[R], const double (&n1)[R], double (&s0)[R],
+                                             double (&s1)[R]);
+
 template <bool FAST, bool CN = false>
 __device__ __forceinline__ void div2(double n0, double n1, double s, double &q0, double &q1) {
   if constexpr (!FAST) {
@@ -152,6 +161,41 @@ __device__ __forceinline__ double clip_c2v(double q) {
     if (q > 1.0 - kSmallestProb) q = 1.0 - kSmallestProb;
     if (q < kSmallestProb) q = kSmallestProb;
     return q;
+  }
+}
+
+template <int R, bool FAST>
+__device__ __forceinline__ void cn_c2v_rows(const double (&t0)[R], const double (&ts)[R], double (&q)[R]) {
+  if constexpr (FAST) {
+    double rc[R];
+    rcp_cn_rows<R>(ts, rc);
+#pragma unroll
+    for (int i = 0; i < R; ++i) q[i] = clip_c2v<true>(qdiv_r(t0[i], ts[i], rc[i]));
+  } else {
+#pragma unroll
+    for (int i = 0; i < R; ++i) q[i] = clip_c2v<false>(t0[i] / ts[i]);
+  }
+}
+template <int R, bool FAST>
+__device__ __forceinline__ void cn_norm_rows(const double (&n0)[R], const double (&n1)[R], double (&s0)[R],
+                                             double (&s1)[R]) {
+  double ns[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) ns[i] = n0[i] + n1[i];
+  if constexpr (FAST) {
+    double rc[R];
+    rcp_cn_rows<R>(ns, rc);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      s0[i] = qdiv_r(n0[i], ns[i], rc[i]);
+      s1[i] = qdiv_r(n1[i], ns[i], rc[i]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      s0[i] = n0[i] / ns[i];
+      s1[i] = n1[i] / ns[i];
+    }
   }
 }
 

@@ -180,7 +180,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
           }
         } else {
           // c2v of edge (odd ? st : DC-1-st) from (own state at DC-1-st, partner state at st)
-          double t0[RC], ts[RC], rc[RC];
+          double t0[RC], ts[RC], q[RC];
 #pragma unroll
           for (int r = 0; r < RC; ++r) {
             const double y0 = swap_pair(s0[r]);
@@ -188,34 +188,21 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
             const double o0 = x0[r][DC - 1 - st], o1 = x1[r][DC - 1 - st];
             const bool unit = FAST && st == DC - 1;  // own state is the boundary (1, 0)
             t0[r] = unit ? y0 : o0 * y0 + o1 * y1;
-            const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
-            ts[r] = t0[r] + t1;
+            ts[r] = t0[r] + (unit ? y1 : o0 * y1 + o1 * y0);
           }
-          if constexpr (FAST) rcp_cn_rows<RC>(ts, rc);  // the sums are within ulps of 1
+          cn_c2v_rows<RC, FAST>(t0, ts, q);  // the sums are within ulps of 1 (bp_common.hpp)
 #pragma unroll
-          for (int r = 0; r < RC; ++r)
-            lds_st<double>(wb[r] + (DC - 1 - st) * 32,
-                           clip_c2v<FAST>(FAST ? qdiv_r(t0[r], ts[r], rc[r]) : div1<false>(t0[r], ts[r])));
+          for (int r = 0; r < RC; ++r) lds_st<double>(wb[r] + (DC - 1 - st) * 32, q[r]);
         }
         if (advance) {
-          double n0[RC], n1[RC], ns[RC], rc[RC];
+          double n0[RC], n1[RC];
 #pragma unroll
           for (int r = 0; r < RC; ++r) {
             const bool unit = FAST && st == 0;  // state (1, 0)
             n0[r] = unit ? m0[r] : s0[r] * m0[r] + s1[r] * m1[r];
             n1[r] = unit ? m1[r] : s0[r] * m1[r] + s1[r] * m0[r];
-            ns[r] = n0[r] + n1[r];
           }
-          if constexpr (FAST) rcp_cn_rows<RC>(ns, rc);
-#pragma unroll
-          for (int r = 0; r < RC; ++r) {
-            if constexpr (FAST) {
-              s0[r] = qdiv_r(n0[r], ns[r], rc[r]);
-              s1[r] = qdiv_r(n1[r], ns[r], rc[r]);
-            } else {
-              div2<false>(n0[r], n1[r], ns[r], s0[r], s1[r]);
-            }
-          }
+          cn_norm_rows<RC, FAST>(n0, n1, s0, s1);
         }
       }
 #pragma unroll
