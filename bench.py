@@ -217,7 +217,7 @@ def main():
         try:
             pm = json.load(open(pmc))
             if (pm.get("batch") == B and pm.get("workload") == args.matrix and not args.blind
-                    and pm.get("kernel") == bp_kernel):
+                    and pm.get("kernel") == bp_kernel.split()[0]):
                 traffic = pm.get("hbm_bytes_per_launch")
                 if pm.get("valu_issue_busy_frac") is not None:
                     issue_view = {
@@ -225,8 +225,9 @@ def main():
                         "valu_wave_instr_per_launch": pm["valu_wave_instr_per_launch"],
                         "rule": "PMC (profiles/pmc_bp.json): SIMD cycles the VALU instruction stream occupies "
                                 "(4 per wave64 instruction, 16 per v_rcp_f64) / SIMD cycles of the launch; the fp64 "
-                                "peak above assumes every instruction is an FMA, this kernel's exact-division "
-                                "arithmetic is 52% FMA, 28% MUL, 13% ADD, 7% rcp",
+                                "peak above assumes every instruction is an FMA; this kernel's exact-division "
+                                "arithmetic is 38% FMA, 32% MUL, 27% ADD, 3% rcp (fp64 instructions, PMC); "
+                                "the CN phase's near-one reciprocals are adds",
                     }
         except Exception:
             traffic = None
