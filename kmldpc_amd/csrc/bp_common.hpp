@@ -39,12 +39,14 @@ __device__ __forceinline__ void lds_st(unsigned a, T v) {
 // with column degree <= 20, which bounds every nonzero message, sum and quotient
 // of the decoder below 1 and above 2^-840 ("Exact fast division").
 // hipcc's reciprocal refinement of an f64 '/': v_rcp_f64 and two Newton steps.
+// (-r) * s + 1 is the same exact product-sum as (-s) * r + 1; negating the
+// per-use operand lets the negation ride on an fma source modifier instead of
+// a materialised -s shared across branches (two VALU moves per sum).
 __device__ __forceinline__ double rcp_refine(double s) {
-  const double ns = -s;
   double r = __builtin_amdgcn_rcp(s);
-  double e = fma(ns, r, 1.0);
+  double e = fma(-r, s, 1.0);
   r = fma(r, e, r);
-  e = fma(ns, r, 1.0);
+  e = fma(-r, s, 1.0);
   return fma(r, e, r);
 }
 
@@ -91,7 +93,7 @@ __device__ __forceinline__ void rcp_cn_rows(const double (&s)[R], double (&r)[R]
 // n / s from a reciprocal r of s that is exact for it (FAST division tail).
 __device__ __forceinline__ double qdiv_r(double n, double s, double r) {
   const double m = n * r;
-  return fma(fma(-s, m, n), r, m);
+  return fma(fma(-m, s, n), r, m);
 }
 
 // One CN step's normalisations for R rows: the c2v quotients clip(t0 / ts)
@@ -109,12 +111,11 @@ __device__ __forceinline__ void div2(double n0, double n1, double s, double &q0,
     q0 = n0 / s;
     q1 = n1 / s;
   } else {
-    const double ns = -s;
     const double r = CN ? rcp_cn(s) : rcp_refine(s);
     const double m0 = n0 * r;
     const double m1 = n1 * r;
-    const double f0 = fma(ns, m0, n0);
-    const double f1 = fma(ns, m1, n1);
+    const double f0 = fma(-m0, s, n0);
+    const double f1 = fma(-m1, s, n1);
     q0 = fma(f0, r, m0);
     q1 = fma(f1, r, m1);
   }
@@ -125,10 +126,9 @@ __device__ __forceinline__ double div1(double n0, double s) {
   if constexpr (!FAST) {
     return n0 / s;
   } else {
-    const double ns = -s;
     const double r = CN ? rcp_cn(s) : rcp_refine(s);
     const double m0 = n0 * r;
-    const double f0 = fma(ns, m0, n0);
+    const double f0 = fma(-m0, s, n0);
     return fma(f0, r, m0);
   }
 }

@@ -22,7 +22,7 @@ __device__ __forceinline__ double prob_clip(double v) {  // utility.cc:18-26
 // or at least 2^-969, the quotient is normal and the exponent gap is below 768.
 __device__ __forceinline__ double qdiv(double n, double s, double r) {
   const double m = n * r;
-  return fma(fma(-s, m, n), r, m);
+  return fma(fma(-m, s, n), r, m);
 }
 
 // Constellation points staged in LDS by the calling kernel (cons_lds); CP is
