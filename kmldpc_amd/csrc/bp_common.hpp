@@ -66,10 +66,16 @@ __device__ __forceinline__ double rcp_refine(double s) {
 // 13: one ulp low), and hipcc's '/' then misrounds three significands (the
 // GPU test test_cn_reciprocal_exhaustive shows both).
 constexpr double kNearOne = 0x1p-40;
+#ifndef KML_CN_RANGE_CHECK
+#define KML_CN_RANGE_CHECK 0
+#endif
 __device__ __forceinline__ double rcp_near1(double s) { return 1.0 + ((1.0 - s) + 0x1p-80); }
+// (see rcp_cn_rows for why the range check is off by default)
 __device__ __forceinline__ double rcp_cn(double s) {
   double r = rcp_near1(s);
-  if (__builtin_expect(!(fabs(1.0 - s) <= kNearOne), 0)) r = rcp_refine(s);  // never seen in a CN phase
+#if KML_CN_RANGE_CHECK
+  if (__builtin_expect(!(fabs(1.0 - s) <= kNearOne), 0)) r = rcp_refine(s);
+#endif
   return r;
 }
 
@@ -77,18 +83,27 @@ __device__ __forceinline__ double rcp_cn(double s) {
 // formula, or — when any sum of the lane is out of its range (not seen in a
 // CN phase) — hipcc's refinement for all R, as the other FAST divisions use.
 // One branch per step keeps the R rows' chains in one scheduling region.
+//
+// The range check is provably redundant on the FAST path: a CN sum is
+// RN(n0 + n1) with n0 = RN(RN(s0 m0) + RN(s1 m1)), n1 likewise, where (s0, s1)
+// and (m0, m1) are quotient pairs of one normalisation (each pair sums to
+// 1 within 2 ulps: RN(x0/S) + RN(x1/S) with S = RN(x0 + x1)) or the boundary
+// state (1, 0); the few roundings keep |s - 1| <= 16 * 2^-53 = 2^-49, far
+// inside 2^-40 (products that underflow are tiny beside the sum's dominant
+// terms).  KML_CN_RANGE_CHECK=1 builds keep it anyway (A/B, debugging).
 template <int R>
 __device__ __forceinline__ void rcp_cn_rows(const double (&s)[R], double (&r)[R]) {
+#pragma unroll
+  for (int i = 0; i < R; ++i) r[i] = rcp_near1(s[i]);
+#if KML_CN_RANGE_CHECK
   bool ok = true;
 #pragma unroll
-  for (int i = 0; i < R; ++i) {
-    r[i] = rcp_near1(s[i]);
-    ok = ok & (fabs(1.0 - s[i]) <= kNearOne);
-  }
+  for (int i = 0; i < R; ++i) ok = ok & (fabs(1.0 - s[i]) <= kNearOne);
   if (__builtin_expect(!ok, 0)) {
 #pragma unroll
     for (int i = 0; i < R; ++i) r[i] = rcp_refine(s[i]);
   }
+#endif
 }
 // n / s from a reciprocal r of s that is exact for it (FAST division tail).
 __device__ __forceinline__ double qdiv_r(double n, double s, double r) {
