@@ -52,7 +52,8 @@ __device__ __forceinline__ double rcp_refine(double s) {
 
 // The reciprocal of a sum within 2^-40 of 1, correctly rounded.  Every
 // normalisation sum of the CN phase is one (s = (s0 + s1)(m0 + m1) of two
-// normalised pairs, within a few ulps of 1).  With u = 1 - s (exact),
+// normalised pairs, within a few ulps of 1), and so is the VN phase's last
+// backward step, whose t is the normalised forward state itself (beta = 1).  With u = 1 - s (exact),
 // 1/s = 1 + u + u^2 + ..., which rounds to 1 + u, except that when 1 + u is a
 // midpoint (s < 1 an odd multiple of 2^-53 below 1) the positive u^2 term
 // rounds it up; 1 + (u + 2^-80) reproduces both (u + 2^-80 is exact, and

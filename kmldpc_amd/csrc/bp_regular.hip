@@ -109,7 +109,10 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
           const double t0 = unit ? al0[r][k] : al0[r][k] * b0[r];
           const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
           double q0, q1;
-          div2<FAST>(t0, t1, t0 + t1, q0, q1);
+          if (unit)  // beta = (1, 1): t is the normalised alpha, its sum within ulps of 1 (bp_common.hpp rcp_near1)
+            div2<FAST, true>(t0, t1, t0 + t1, q0, q1);
+          else
+            div2<FAST>(t0, t1, t0 + t1, q0, q1);
           lds_st<dbl2>(vaddr[r][k] & ~15u, dbl2{q0, q1});
           if (k > 0) {
             const double c0 = c0s[r][k];
