@@ -14,6 +14,8 @@
 
 #include <cstdint>
 
+#include "layout.hpp"  // kIrrThreads, kIrrVnPairMax, kIrrCnPairMax
+
 namespace kml {
 
 // Device-resident code description (uploaded once per context).
@@ -77,9 +79,6 @@ struct BpLaunch {
 };
 
 hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s);
-constexpr int kIrrThreads = 768;  // threads per workgroup of bp_irregular.hip (its plan is made for this)
-constexpr int kIrrVnPairMax = 4;  // highest column degree bp_irregular.hip pairs
-constexpr int kIrrCnPairMax = 8;  // highest row degree it pairs
 hipError_t launch_bp_irregular(const DevCode &c, const BpLaunch &a, hipStream_t s);
 // Cooperative kernel for regular codes whose slots exceed the LDS: groups of
 // workgroups on one XCD share a codeword.  0 groups = not applicable.

@@ -81,6 +81,11 @@ namespace kml {
 // most from a second chain; the limits keep two chains within the registers), and the waves are placed so that the modelled VALU work of
 // the 4 SIMDs (wave w runs on SIMD w % 4) is balanced.  Any placement gives
 // the same decoder output: it only moves work between lanes.
+constexpr int kIrrThreads = 768;  // threads per workgroup of bp_irregular.hip (its plan is made for this)
+constexpr int kIrrVnPairMax = 4;  // highest column degree bp_irregular.hip pairs
+constexpr int kIrrCnPairMax = 8;  // highest row degree it pairs (BG2, 50 iterations: 4/8 19.7 ms,
+                                  // 5/8 20.5, 7/8 21.8, 9/8 23.0 with c2v reloads against spills)
+
 struct IrregularPlan {
   std::vector<int32_t> vn;  // [3*T]: column of position r*T + t, -1 = idle
   std::vector<int32_t> cn;  // [3*T/2]: row of lane pair r*T/2 + (t >> 1), -1 = idle

@@ -186,6 +186,23 @@ def test_log_host_restatement(tmp_path):
     assert "log_fma_mismatch=0" in out.stdout
 
 
+def test_kernel_placement_plans(tmp_path, data_dir):
+    """The lane / slot placement plans the kernels rely on (layout.cpp), on the
+    reference's H files: bp_regular's interleaved row slots and c2v halves,
+    bp_irregular's paired rounds (each column / row once, pairs of one degree
+    within the limits, one degree per paired wave), bp_part's partition."""
+    exe = tmp_path / "planc"
+    csrc = os.path.join(REPO, "kmldpc_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", csrc, "-o", str(exe),
+                    os.path.join(REPO, "tests", "native", "plan_check.cpp"), os.path.join(csrc, "code.cpp"),
+                    os.path.join(csrc, "layout.cpp")], check=True)
+    out = subprocess.run([str(exe)] + [os.path.join(data_dir, f) for f in
+                                       ("PEG2304regular0.5.txt", "5GLDPCBG2a3_R12_K960.txt", "PEG8064regular0.5.txt")],
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    assert "plan_errors=0" in out.stdout
+
+
 # ---------------------------------------------------------- host random sources
 def test_reference_rngs_match_reference():
     """CLCRandNum / CWHRandNum / GetSymStr / GetBitStr with SetSeed(-1) equal the
