@@ -5,6 +5,7 @@ bit-identical to the oracle, and the exact-math restatements used by the
 device code equal glibc / libgcc on the host."""
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -201,6 +202,16 @@ def test_kernel_placement_plans(tmp_path, data_dir):
                          capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
     assert "plan_errors=0" in out.stdout
+
+
+def test_cn_division_tail_exact_near_one():
+    """The CN phases' division (near-one reciprocal RN(1/s), then the FAST
+    tail) rounds n / s correctly on every significand where it could fail, for
+    |s - 1| <= 64 ulp: exact rational evaluation (tools/verify_cn_division.py)."""
+    out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "verify_cn_division.py")],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout
+    assert "near-one reciprocal misses: 0" in out.stdout
 
 
 # ---------------------------------------------------------- host random sources
