@@ -57,8 +57,8 @@ __device__ __forceinline__ double rcp_refine(double s) {
 // 1/s = 1 + u + u^2 + ..., which rounds to 1 + u, except that when 1 + u is a
 // midpoint (s < 1 an odd multiple of 2^-53 below 1) the positive u^2 term
 // rounds it up; 1 + (u + 2^-80) reproduces both (u + 2^-80 is exact, and
-// 2^-80 breaks exactly the ties u^2 breaks).  So rcp_near1(s) = RN(1/s): three
-// adds instead of a quarter-rate v_rcp_f64 and four fmas.  With a correctly
+// 2^-80 breaks exactly the ties u^2 breaks).  So rcp_near1(s) = RN(1/s): two
+// instructions instead of a quarter-rate v_rcp_f64 and four fmas.  With a correctly
 // rounded reciprocal the division tail (m = RN(n r), q = fma(fma(-s, m, n), r,
 // m)) is off only when n / s lies within 2^-51 ulp of a rounding midpoint;
 // tools/verify_cn_division.py enumerates every such n for |s - 1| <= 64 ulp
@@ -70,7 +70,10 @@ constexpr double kNearOne = 0x1p-40;
 #ifndef KML_CN_RANGE_CHECK
 #define KML_CN_RANGE_CHECK 0
 #endif
-__device__ __forceinline__ double rcp_near1(double s) { return 1.0 + ((1.0 - s) + 0x1p-80); }
+// Two instructions: X * Y = 1 + 2^-78 exactly (X = 1 + 2^-26, Y = 1 - 2^-26 +
+// 2^-52), so fma(X, Y, 1 - s) is RN(1 + u + 2^-78) with one rounding — the
+// same tie-breaking as 1 + (u + 2^-80) without the third add.
+__device__ __forceinline__ double rcp_near1(double s) { return fma(0x1.0000004p+0, 0x1.ffffff8000002p-1, 1.0 - s); }
 // (see rcp_cn_rows for why the range check is off by default)
 __device__ __forceinline__ double rcp_cn(double s) {
   double r = rcp_near1(s);
