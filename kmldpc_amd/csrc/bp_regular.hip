@@ -30,7 +30,10 @@
 //     upper half of its slot by bit 2 of the row's CN position.  The VN phase
 //     reads it at the planned byte offset.
 //   * every LDS address is kept absolute in a register (bp_common.hpp lds_ld).
+#include <cstdlib>
+
 #include "bp_common.hpp"
+#include "demap_common.hpp"
 #include "kernels.hpp"
 
 namespace kml {
@@ -225,9 +228,21 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
   conv_out = conv;
 }
 
-template <int T, int RV, int RC, int DV, int DC, bool SYN>
+// Dynamic LDS: E slots of 16 B, the reduction words, N hard-decision bytes,
+// then (fused demap only, 16-byte aligned) the codeword's N priors.
+constexpr size_t p0s_offset(int E, int N) { return ((size_t)E * 16 + kRedBytes + (size_t)N + 15) & ~(size_t)15; }
+
+template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB>
 __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, unsigned int *queue, int fast_allowed) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // fused demap: the constellation and the exp table in LDS (demap_common.hpp)
+  __shared__ double dcons[DMB > 0 ? (2 << DMB) : 2];
+  __shared__ uint64_t detab[DMB > 0 ? 256 : 1];
+  double *p0s = reinterpret_cast<double *>(smem + p0s_offset(c.E, c.N));
+  if constexpr (DMB > 0) {
+    for (int k = threadIdx.x; k < (2 << DMB); k += T) dcons[k] = a.sym_cons[k];
+    stage_exp_table(detab);
+  }
   constexpr int H = (DC + 1) / 2;
   const int tid = threadIdx.x;
   const int odd = tid & 1;
@@ -281,8 +296,24 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
     const int entry = red[3];
     if (entry >= a.B) break;
     const int cw = a.cw_idx ? a.cw_idx[entry] : entry;
-    const double *p0 = a.p0 + (long long)cw * a.p0_stride;
-    if (a.p0_sel) p0 += (long long)a.p0_sel[cw] * a.p0_sel_stride;
+    const double *p0;
+    if constexpr (DMB > 0) {  // ModemLinearSystem::DeMapping of this codeword into LDS
+      const int S = c.cc_len / DMB;
+      const double2 hh = a.sym_h[cw];
+      const double2 *yy = a.sym_y + (long long)cw * S;
+      for (int j = tid; j < S; j += T) {
+        const double2 v = yy[j];
+        double out[DMB];
+        demap_symbol<DMB>((lds_cons)dcons, (lds_exptab)detab, v.x, v.y, hh.x, hh.y, a.sym_var, out);
+#pragma unroll
+        for (int b = 0; b < DMB; ++b) p0s[j * DMB + b] = out[b];
+      }
+      __syncthreads();
+      p0 = p0s;
+    } else {
+      p0 = a.p0 + (long long)cw * a.p0_stride;
+      if (a.p0_sel) p0 += (long long)a.p0_sel[cw] * a.p0_sel_stride;
+    }
 
     double pv[RV];
     bool ok = true;
@@ -360,10 +391,10 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
   }
 }
 
-template <int T, int RV, int RC, int DV, int DC, bool SYN>
+template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB>
 hipError_t launch_reg_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
-  auto kern = bp_regular_kernel<T, RV, RC, DV, DC, SYN>;
-  const size_t lds = (size_t)c.E * 16 + kRedBytes + (size_t)c.N;
+  auto kern = bp_regular_kernel<T, RV, RC, DV, DC, SYN, DMB>;
+  const size_t lds = DMB > 0 ? p0s_offset(c.E, c.N) + (size_t)c.N * 8 : (size_t)c.E * 16 + kRedBytes + (size_t)c.N;
   hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   int dev = 0, ncu = 0;
@@ -390,7 +421,20 @@ hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s)
   if (!c.reg_c2v || bp_regular_threads(c.N, c.M, c.E, c.dv_max, c.dc_max, c.regular) != 768)
     return hipErrorNotSupported;
   const int fast = c.dv_max <= kFastMaxColumnDegree ? 1 : 0;
-  return a.syn ? launch_reg_t<768, 3, 3, 3, 6, true>(c, a, s, fast) : launch_reg_t<768, 3, 3, 3, 6, false>(c, a, s, fast);
+  if (a.sym_y) {
+    if (!bp_regular_fuses_demap(c, a.sym_bits) || a.cw_idx || a.p0_sel) return hipErrorNotSupported;
+    return a.syn ? launch_reg_t<768, 3, 3, 3, 6, true, 2>(c, a, s, fast)
+                 : launch_reg_t<768, 3, 3, 3, 6, false, 2>(c, a, s, fast);
+  }
+  return a.syn ? launch_reg_t<768, 3, 3, 3, 6, true, 0>(c, a, s, fast)
+               : launch_reg_t<768, 3, 3, 3, 6, false, 0>(c, a, s, fast);
+}
+
+bool bp_regular_fuses_demap(const DevCode &c, int bits) {
+  if (const char *e = getenv("KML_FUSED_DEMAP"))
+    if (e[0] == '0') return false;
+  return c.reg_c2v && bp_regular_threads(c.N, c.M, c.E, c.dv_max, c.dc_max, c.regular) == 768 && c.punct == 0 &&
+         bits == 2 && c.cc_len % bits == 0 && p0s_offset(c.E, c.N) + (size_t)c.N * 8 <= 160 * 1024;
 }
 
 }  // namespace kml

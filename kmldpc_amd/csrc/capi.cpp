@@ -485,6 +485,15 @@ int receive(kml_ctx *c, const RecvIO &io, double snr, int B, int &bp_slot) {
   a.ret = io.ret;
   a.ref_bits = io.ref_bits;
   a.cw_err = io.cw_err;
+  if (io.true_h && !io.histogram && kml::bp_regular_fuses_demap(c->dc, c->modem.bits)) {
+    // known channel on the regular kernel: the demap runs in its prologue
+    a.sym_y = io.y;
+    a.sym_h = io.true_h;
+    a.sym_cons = cons;
+    a.sym_var = var;
+    a.sym_bits = c->modem.bits;
+    return run_bp(c, a, bp_slot);
+  }
   if (io.true_h && !io.histogram) {  // known channel: one demap + BP
     HIPCHK(c, c->w_p0.ensure(sizeof(double) * cc * B), "hipMalloc(p0)");
     Timer t(c, "demap", -1, (double)B * S * (16.0 + 8.0 * c->modem.bits));

@@ -76,9 +76,19 @@ struct BpLaunch {
   double2 *gslots = nullptr;     // global slot scratch when E*16 exceeds LDS
   long long gslots_cap = 0;      // number of double2 available
   unsigned int *queue = nullptr; // 4-byte device dequeue counter (zeroed by the launcher)
+  // Fused demap (bp_regular.hip only, bp_regular_fuses_demap): when sym_y is
+  // set, p0 is ignored and each codeword's P0 is computed in the kernel's
+  // prologue from y[B][S] and the known channel h[B] (demap_common.hpp).
+  const double2 *sym_y = nullptr;
+  const double2 *sym_h = nullptr;
+  const double *sym_cons = nullptr;  // the normalised constellation, 2 << bits doubles
+  double sym_var = 0;
+  int sym_bits = 0;
 };
 
 hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s);
+// Can the regular kernel compute P0 itself (BpLaunch::sym_y) for this code and modem?
+bool bp_regular_fuses_demap(const DevCode &c, int bits);
 hipError_t launch_bp_irregular(const DevCode &c, const BpLaunch &a, hipStream_t s);
 // Cooperative kernel for regular codes whose slots exceed the LDS: groups of
 // workgroups on one XCD share a codeword.  0 groups = not applicable.
