@@ -265,7 +265,8 @@ def main():
             "avg_launch_ms": round(bp_avg_ms, 4),
             "alg_flops_per_launch": round(bp_flops),
             "alg_flops_rule": "per executed VN phase sum_cols (68*d-23), per CN phase sum_rows (73*d-52) fp64 flops "
-                              "(DESIGN.md: Roofline)",
+                              "(DESIGN.md: Roofline); known-channel QPSK launches also run the demap in their "
+                              "prologue, whose work is not counted (conservative)",
             "issue_view": issue_view,
             "hbm_view": {
                 "alg_bytes_per_launch": round(bp_bytes),
