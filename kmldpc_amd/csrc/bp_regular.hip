@@ -299,7 +299,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
     const double *p0;
     if constexpr (DMB > 0) {  // ModemLinearSystem::DeMapping of this codeword into LDS
       const int S = c.cc_len / DMB;
-      const double2 hh = a.sym_h[cw];
+      const double2 hh = a.sym_h[(long long)cw * a.sym_h_stride + (a.sym_h_sel ? a.sym_h_sel[cw] : 0)];
       const double2 *yy = a.sym_y + (long long)cw * S;
       for (int j = tid; j < S; j += T) {
         const double2 v = yy[j];

@@ -558,6 +558,16 @@ int receive(kml_ctx *c, const RecvIO &io, double snr, int B, int &bp_slot) {
       if (io.uh) HIPCHK(c, hipMemsetAsync(io.uh, 0, (size_t)B * K, c->stream), "memset uh");
       return KML_OK;
     }
+    if (kml::bp_regular_fuses_demap(c->dc, c->modem.bits)) {  // demap with the chosen estimate in the BP prologue
+      a.sym_y = io.y;
+      a.sym_h = hc;
+      a.sym_h_stride = nc;
+      a.sym_h_sel = chosen;
+      a.sym_cons = cons;
+      a.sym_var = var;
+      a.sym_bits = c->modem.bits;
+      return run_bp(c, a, bp_slot);
+    }
     HIPCHK(c, c->w_p0.ensure(sizeof(double) * cc * B), "hipMalloc(p0)");
     Timer t2(c, "demap", -1, (double)B * S * (16.0 + 8.0 * c->modem.bits));
     HIPCHK(c, kml::launch_demap(c->modem.bits, cons, io.y, S, 1, hc, nc, chosen, var, B, c->w_p0.as<double>(),

@@ -80,7 +80,9 @@ struct BpLaunch {
   // set, p0 is ignored and each codeword's P0 is computed in the kernel's
   // prologue from y[B][S] and the known channel h[B] (demap_common.hpp).
   const double2 *sym_y = nullptr;
-  const double2 *sym_h = nullptr;
+  const double2 *sym_h = nullptr;     // h of codeword cw: sym_h[cw * sym_h_stride + (sym_h_sel ? sym_h_sel[cw] : 0)]
+  int sym_h_stride = 1;
+  const int32_t *sym_h_sel = nullptr;  // chosen candidate (blind path)
   const double *sym_cons = nullptr;  // the normalised constellation, 2 << bits doubles
   double sym_var = 0;
   int sym_bits = 0;
