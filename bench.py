@@ -226,7 +226,7 @@ def main():
                         "rule": "PMC (profiles/pmc_bp.json): SIMD cycles the VALU instruction stream occupies "
                                 "(4 per wave64 instruction, 16 per v_rcp_f64) / SIMD cycles of the launch; the fp64 "
                                 "peak above assumes every instruction is an FMA; this kernel's exact-division "
-                                "arithmetic is 42% FMA, 34% MUL, 20% ADD, 3% rcp (fp64 instructions, PMC); "
+                                "arithmetic is 43% FMA, 34% MUL, 21% ADD, 3% rcp (fp64 instructions, PMC, incl. the fused demap); "
                                 "the CN phase's near-one reciprocals are adds",
                     }
         except Exception:
