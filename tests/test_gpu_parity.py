@@ -307,6 +307,25 @@ def test_demap_and_metric_adversarial(data_dir, matrix, modem, snr):
         assert out["metrics"][i][0] == abs(oc.parity_count(rr)), i
 
 
+@pytest.mark.parametrize("blind", [False, True])
+def test_fused_demap_matches_separate(data_dir, blind, monkeypatch):
+    """Known-channel and chosen-candidate QPSK decodes on the regular code run
+    the demap in the BP kernel's prologue; KML_FUSED_DEMAP=0 runs the separate
+    demap kernel: every output is identical (and the oracle agrees)."""
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    oc = oracle_for(data_dir, "PEG2304regular0.5.txt", False)
+    om = O.Modem(os.path.join(data_dir, "2bits_QPSK.txt"))
+    uu, cc, th, y = O.gen_frames(oc, om, 2.0, 96, state=23)
+    r1 = ctx.decode_frames(y, 2.0, None if blind else th)
+    monkeypatch.setenv("KML_FUSED_DEMAP", "0")
+    r0 = ctx.decode_frames(y, 2.0, None if blind else th)
+    for k in ("uu_hat", "chosen", "ret", "metrics"):
+        assert np.array_equal(r1[k], r0[k]), k
+    for i in range(0, 96, 8):
+        ref = O.receive(oc, om, y[i], th[i], 2.0, blind)
+        assert np.array_equal(r1["uu_hat"][i], ref["uu_hat"]) and r1["ret"][i] == ref["ret"], i
+
+
 @pytest.mark.parametrize("matrix,modem,snr,n", [
     ("PEG2304regular0.5.txt", "2bits_QPSK.txt", 2.0, 200),
     ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", 5.01, 100),
