@@ -236,4 +236,26 @@ __device__ __forceinline__ int hard_decision(double n0, double n1) {
   return (a0 > a1) ? 0 : 1;
 }
 
+// SourceSink::CntErr (sourcesink.cc:29-47) of one codeword's info bits against
+// its packed source word array ref[Kw]: Σ popcount(packed(uu_hat) ^ ref).
+// Wave w of the workgroup packs words w, w + T/64, ... with one ballot each
+// (lane j holds bit 64w + j, zero past K), so the 64-step serial pack of the
+// one-thread-per-word form leaves the codeword's tail.  cch holds 0/1 hard
+// decisions; bit i sits at cch[pos ? pos[off + i] : off + i].  Returns the
+// wave's count on lane 0, 0 on the other lanes.
+template <int T>
+__device__ __forceinline__ int count_info_errors(const unsigned char *cch, const int *pos, int off, int K, int Kw,
+                                                 const uint64_t *ref, int tid) {
+  const int lane = tid & 63;
+  int errs = 0;
+  for (int w = tid >> 6; w < Kw; w += T / 64) {
+    const int i = w * 64 + lane;
+    int bit = 0;
+    if (i < K) bit = cch[pos ? pos[off + i] : off + i];
+    const uint64_t word = __ballot(bit);
+    if (lane == 0) errs += __popcll(word ^ ref[w]);
+  }
+  return errs;
+}
+
 }  // namespace kml

@@ -356,15 +356,8 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
         if (cnt) atomicAdd(&red[0], cnt);
       }
       if (a.ref_bits) {
-        const uint64_t *ref = a.ref_bits + (long long)cw * c.Kw;
-        int errs = 0;
-        for (int w = tid; w < c.Kw; w += T) {
-          uint64_t word = 0;
-          const int base = w * 64;
-          const int nb = min(64, c.K - base);
-          for (int j = 0; j < nb; ++j) word |= (uint64_t)cch[c.reg_pos[c.info_off + base + j]] << j;
-          errs += __popcll(word ^ ref[w]);
-        }
+        const int errs =
+            count_info_errors<T>(cch, c.reg_pos, c.info_off, c.K, c.Kw, a.ref_bits + (long long)cw * c.Kw, tid);
         if (errs) atomicAdd(&red[1], errs);
       }
     }
