@@ -9,15 +9,32 @@ counting) over the whole resident batch, i.e. KmCodec::Decoder + SourceSink::Cnt
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--blind]
 
-N > 1 is launched by torch.distributed.run, one process per GPU; frames are
-sharded by global codeword index (weak scaling, no data-path collective) and
-the error counters are summed with one RCCL all-reduce at the end.
-Rank 0 prints ONE JSON line.
+--gpus N > 1 without a torch.distributed environment starts
+`python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child
+process (before anything here touches the GPU), forwards rank 0's JSON line
+and exits with the child's status.  Each rank is one process on one GPU;
+frames are sharded by global codeword index (weak scaling, no data-path
+collective) and the error counters are summed with one RCCL all-reduce at the
+end (simulator.cc:35-42, :86-100 run SNR points / codeword chunks as
+independent tasks the same way).  Rank 0 prints ONE JSON line.
+
+Besides the timed region the line carries, all untimed:
+  * stats.ber_match: the first B_ref codewords of the reference's own seed-17
+    stream (CLCRandNum::SetSeed(-1)) decoded on the GPU, compared codeword by
+    codeword with the reference's SourceSink::CntErr counters for the same
+    codewords (tests/golden/bench/*.npz, made by running the reference itself);
+    and the timed Philox batch's BER against the reference BER with its
+    standard error (ber_within_1sigma);
+  * full_loop: GPU frame generation + decode rate (kml_sim_generate + decode);
+  * cpu_baseline: the bit-exact C restatement on the host cores (rank 0, N=1).
 """
 import argparse
 import gzip
+import hashlib
 import json
+import math
 import os
+import socket
 import subprocess
 import sys
 import tempfile
@@ -26,9 +43,7 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-import kmldpc_amd as K  # noqa: E402
-
-K.lib()  # load the HIP library (and its ROCm runtime) before torch
+K = None  # kmldpc_amd, imported only in a rank process (after the launch decision)
 
 KERNEL_NOTES = {
     "bp_regular_kernel": "sum-product BP, messages LDS-resident",
@@ -39,6 +54,17 @@ KERNEL_NOTES = {
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 dense peak (vector = matrix rate, AMD spec)
+# sources whose code the PMC summary describes (profiles/pmc_bp.json src_sha)
+PMC_SOURCES = ["bp_regular.hip", "bp_common.hpp", "demap_common.hpp", "exact_math.hpp", "kernels.hpp",
+               "layout.cpp", "capi.cpp"]
+
+
+def src_sha():
+    h = hashlib.sha256()
+    for fn in PMC_SOURCES:
+        with open(os.path.join(REPO, "kmldpc_amd", "csrc", fn), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def data_dir():
@@ -79,22 +105,38 @@ def write_config(d, args):
     return cfg
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of quota from cgroup v2 cpu.max (None = unlimited / unknown)."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(d, args):
     """The oracle restatement of the same receive path timed on host cores
-    (reported baseline; test infrastructure, never the measured product)."""
+    (reported baseline; test infrastructure, never the measured product).
+    T = every CPU in sched_getaffinity (BASELINE.md's plan), lowered to the
+    cgroup CPU quota when one is set (threads beyond it only time-slice)."""
     exe = os.path.join(REPO, "oracle", "cpu_baseline")
     if not os.path.exists(exe):
         return None
     try:
-        cores = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
-    n = args.cpu_cw_per_thread
+        affinity = os.cpu_count() or 1
+    quota = cgroup_cpu_quota()
+    threads = affinity if quota is None else max(1, min(affinity, int(math.ceil(quota))))
+    # bounded sample: ~args.cpu_seconds of decode at ~1000 cw/s per thread (known H; blind ~1/2)
+    per_thread_rate = 500.0 if args.blind else 1000.0
+    if args.matrix.startswith("PEG8064") or args.is5g:
+        per_thread_rate /= 8.0
+    n = args.cpu_cw_per_thread or max(50, int(args.cpu_seconds * per_thread_rate))
     cmd = [exe, os.path.join(d, args.matrix), os.path.join(d, args.modem), str(int(args.is5g)), repr(args.snr),
            str(args.max_iter), str(int(args.blind)), str(n), str(threads)]
     try:
-        out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
         r = json.loads(out.stdout.strip().splitlines()[-1])
     except Exception as e:  # pragma: no cover
         print(f"cpu_baseline failed: {e}", file=sys.stderr)
@@ -108,10 +150,69 @@ def cpu_baseline(d, args):
     except OSError:
         pass
     return {"value": round(r["cw_per_s"], 3), "unit": "codewords/s", "cores": threads, "kind": "port",
-            "sample": f"{r['codewords']} codewords ({n}/thread x {threads} threads) of the same workload through "
-                      f"oracle/ (C restatement of KmCodec::Decoder + CntErr, bit-exact vs reference), "
-                      f"{r['seconds']:.1f} s; FER {r['fer']:.4f}",
+            "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "full_loop_value": round(r["full_loop_cw_per_s"], 3),
+            "sample": f"{r['codewords']} codewords ({n}/thread x {threads} threads, one Park-Miller stream per "
+                      f"thread) of the same workload through oracle/ (C restatement of KmCodec::Decoder + CntErr, "
+                      f"bit-exact vs reference): decode {r['seconds']:.1f} s (value), + frame generation "
+                      f"{r['gen_seconds']:.1f} s (full_loop_value); FER {r['fer']:.4f}",
             "cpu_model": cpu_model}
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """Run this script under torch.distributed.run with n ranks as a CHILD
+    process (no exec: nothing in this process has touched the GPU), forward
+    rank 0's JSON line to stdout and return the child's exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    for line in p.stdout.splitlines():
+        if line.startswith('{"metric"'):
+            print(line, flush=True)
+        elif line.strip():
+            print(line, file=sys.stderr)
+    return p.returncode
+
+
+def bench_fixture(args):
+    """The reference's counters for the first B_ref seed-17 codewords of this
+    workload (tests/golden/bench/, generated by oracle/_ref), or None."""
+    import numpy as np
+
+    d = os.path.join(REPO, "tests", "golden", "bench")
+    if not os.path.isdir(d):
+        return None
+    for fn in sorted(os.listdir(d)):
+        if not fn.endswith(".npz"):
+            continue
+        z = np.load(os.path.join(d, fn))
+        hdr = json.loads(bytes(z["hdr_json"]).decode())
+        if (hdr["matrix"] == args.matrix and hdr["modem"] == args.modem and hdr["is5g"] == args.is5g
+                and hdr["known"] == (not args.blind) and hdr["max_iter"] == args.max_iter
+                and abs(hdr["snr"] - args.snr) < 1e-12):
+            return fn, hdr, z["errs"].astype(np.int64)
+    return None
+
+
+def ber_sigma(sum_e, sum_e2, n, Kbits):
+    """Standard error of a BER estimate from per-codeword error counts (the
+    bit errors of one codeword are not independent, so the codeword is the unit)."""
+    if n < 2:
+        return float("nan")
+    mean = sum_e / n
+    var = max(sum_e2 / n - mean * mean, 0.0) * n / (n - 1)
+    return math.sqrt(var / n) / Kbits
 
 
 def main():
@@ -127,18 +228,32 @@ def main():
     ap.add_argument("--is5g", action="store_true")
     ap.add_argument("--blind", action="store_true")
     ap.add_argument("--seed", type=int, default=17)
-    ap.add_argument("--cpu-cw-per-thread", type=int, default=5000)
+    ap.add_argument("--cpu-cw-per-thread", type=int, default=0, help="0: sized for --cpu-seconds")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ber-match", action="store_true")
+    ap.add_argument("--full-loop-batches", type=int, default=3)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI, the production path) or gloo (CPU counters; lets N ranks share "
                          "fewer GPUs for testing)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+
+    global K
+    import kmldpc_amd as K  # noqa: E402
+
+    K.lib()  # load the HIP library (and its ROCm runtime) before torch
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
     device = local
+    ranks_seen = 1
     if world > 1:
         import torch
         import torch.distributed as dist_mod
@@ -150,6 +265,9 @@ def main():
             device = local % max(torch.cuda.device_count(), 1)
             dist_mod.init_process_group(backend="gloo")
         dist = dist_mod
+        ranks_seen = dist.get_world_size()
+
+    import numpy as np
 
     d = data_dir()
     cfg = write_config(d, args)
@@ -181,22 +299,37 @@ def main():
     bp = ctx.prof_read("bp")
     bp_kernel = ctx.bp_kernel()
     stages = {s: ctx.prof_read(s) for s in ("demap", "kmeans", "metric")}
-    # one more (untimed) pass for the statistical counters
-    c = ctx.sim_decode(args.snr, blind=args.blind)
+    # one more (untimed) pass for the statistical counters and per-codeword errors
+    cw_err, _, c = ctx.sim_decode_ex(args.snr, blind=args.blind)
+    e64 = cw_err.astype(np.float64)
+    vals = np.array([c["err_bit"], c["err_blk"], c["tot_bit"], c["tot_blk"], c["vn_phases"], c["cn_phases"],
+                     e64.sum(), (e64 * e64).sum()], dtype=np.float64)
 
-    import numpy as np
-    vals = np.array([c["err_bit"], c["err_blk"], c["tot_bit"], c["tot_blk"], c["vn_phases"], c["cn_phases"]],
-                    dtype=np.float64)
-    t_max = elapsed
+    # full loop (untimed by the headline): GPU frame generation + decode, fresh frames per batch
+    fl_n = max(0, args.full_loop_batches)
+    fl_t = 0.0
+    if fl_n:
+        barrier()
+        tf = time.perf_counter()
+        for i in range(fl_n):
+            ctx.sim_generate(args.snr, B, seed=args.seed + 1, first_cw=(i * world + rank) * B)
+            ctx.sim_decode(args.snr, blind=args.blind, sync=False)
+        barrier()
+        fl_t = time.perf_counter() - tf
+
+    t_max, fl_max, per_rank = elapsed, fl_t, [elapsed]
     if dist is not None:
         import torch
         dev = "cuda" if args.dist_backend == "nccl" else "cpu"
         tv = torch.tensor(vals, device=dev)
         dist.all_reduce(tv)  # RCCL over xGMI: the only collective
         vals = tv.cpu().numpy()
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
+        tt = torch.tensor([elapsed, fl_t], device=dev, dtype=torch.float64)
+        gathered = [torch.zeros_like(tt) for _ in range(ranks_seen)]
+        dist.all_gather(gathered, tt)
+        per_rank = [float(g[0].item()) for g in gathered]
+        t_max = max(per_rank)
+        fl_max = max(float(g[1].item()) for g in gathered)
 
     if rank != 0:
         if dist is not None:
@@ -204,33 +337,81 @@ def main():
         return
     total_cw = B * args.steps * world
     value = total_cw / t_max
-    err_bit, err_blk, tot_bit, tot_blk, vn, cn = vals
+    err_bit, err_blk, tot_bit, tot_blk, vn, cn, sum_e, sum_e2 = vals
+    Kbits = tot_bit / max(tot_blk, 1)
     bp_avg_ms = bp["ms"] / max(bp["launches"], 1)
     bp_bytes = bp["bytes"] / max(bp["launches"], 1)
     bp_flops = bp["flops"] / max(bp["launches"], 1)
     achieved_gbs = bp_bytes / (bp_avg_ms * 1e-3) / 1e9 if bp_avg_ms > 0 else 0.0
     achieved_tf = bp_flops / (bp_avg_ms * 1e-3) / 1e12 if bp_avg_ms > 0 else 0.0
-    traffic = None
-    issue_view = None
+
+    # PMC summary of the same kernel/workload (profiles/pmc_bp.json, tools/pmc_summary.py)
+    traffic, issue_view, frac_exec, pmc_note = None, None, None, "no PMC summary for this kernel/workload"
     pmc = os.path.join(REPO, "profiles", "pmc_bp.json")
     if os.path.exists(pmc):
         try:
             pm = json.load(open(pmc))
             if (pm.get("batch") == B and pm.get("workload") == args.matrix and not args.blind
                     and pm.get("kernel") == bp_kernel.split()[0]):
+                current = pm.get("src_sha") == src_sha()
+                pmc_note = (f"profiles/pmc_bp.json ({pm.get('round', '?')}), "
+                            + ("taken at these kernel sources" if current else
+                               "STALE: taken at other kernel sources (src_sha differs)"))
                 traffic = pm.get("hbm_bytes_per_launch")
+                if pm.get("fp64_flops_executed_per_launch"):
+                    fe = pm["fp64_flops_executed_per_launch"]
+                    frac_exec = {"fp64_flops_executed_per_launch": fe,
+                                 "achieved": round(fe / (bp_avg_ms * 1e-3) / 1e12, 2),
+                                 "frac": round(fe / (bp_avg_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4),
+                                 "rule": "64 x SQ_INSTS_VALU_FLOPS_FP64 per launch (PMC) / this run's avg launch time"}
                 if pm.get("valu_issue_busy_frac") is not None:
-                    issue_view = {
-                        "valu_issue_busy_frac": pm["valu_issue_busy_frac"],
-                        "valu_wave_instr_per_launch": pm["valu_wave_instr_per_launch"],
-                        "rule": "PMC (profiles/pmc_bp.json): SIMD cycles the VALU instruction stream occupies "
-                                "(4 per wave64 instruction, 16 per v_rcp_f64) / SIMD cycles of the launch; the fp64 "
-                                "peak above assumes every instruction is an FMA; this kernel's exact-division "
-                                "arithmetic is 43% FMA, 34% MUL, 21% ADD, 3% rcp (fp64 instructions, PMC, incl. the fused demap); "
-                                "the CN phase's near-one reciprocals are adds",
-                    }
+                    issue_view = {"valu_issue_busy_frac": pm["valu_issue_busy_frac"],
+                                  "valu_wave_instr_per_launch": pm["valu_wave_instr_per_launch"],
+                                  "rule": "SIMD cycles the VALU instruction stream occupies (4 per wave64 "
+                                          "instruction, 16 per v_rcp_f64) / SIMD cycles of the launch"}
         except Exception:
             traffic = None
+
+    stats = {
+        "fer": err_blk / max(tot_blk, 1),
+        "ber": err_bit / max(tot_bit, 1),
+        "ber_sigma": ber_sigma(sum_e, sum_e2, tot_blk, Kbits),
+        "codewords": int(tot_blk),
+        "mean_cn_phases": cn / max(tot_blk, 1),
+        "mean_vn_phases": vn / max(tot_blk, 1),
+        "stage_ms_per_step": {s: round(v["ms"] / max(args.steps, 1), 4) for s, v in stages.items() if v["launches"]},
+        "bp_ms_per_step": round(bp["ms"] / max(args.steps, 1), 4),
+    }
+    fx = None if args.no_ber_match else bench_fixture(args)
+    if fx is not None:
+        fn, hdr, ref_errs = fx
+        n_ref = int(hdr["n"])
+        # (1) the reference's own stream through the GPU path, codeword by codeword
+        rng = K.CLCRandNum(hdr.get("seed", 17))
+        uu, th, y = ctx.ref_frames(rng, args.snr, n_ref)
+        ctx.sim_load(args.snr, uu, y, th)
+        del y
+        g_err, _, gc = ctx.sim_decode_ex(args.snr, blind=args.blind)
+        same = bool(np.array_equal(g_err.astype(np.int64), ref_errs))
+        ref_bit, ref_blk = int(ref_errs.sum()), int((ref_errs > 0).sum())
+        r_e = ref_errs.astype(np.float64)
+        ber_ref = ref_bit / (n_ref * hdr["K"])
+        sig_ref = ber_sigma(r_e.sum(), (r_e * r_e).sum(), n_ref, hdr["K"])
+        # (2) the timed (Philox) batch vs the reference, Monte-Carlo standard errors
+        sig = math.hypot(sig_ref, stats["ber_sigma"])
+        z = (stats["ber"] - ber_ref) / sig if sig > 0 else float("nan")
+        stats.update({
+            "ber_ref": ber_ref, "fer_ref": ref_blk / n_ref, "ber_ref_sigma": sig_ref,
+            "ber_z": z, "ber_sigma_combined": sig, "ber_within_1sigma": bool(abs(z) <= 1.0),
+            "ber_match": {
+                "frames": f"reference stream CLCRandNum seed 17, first {n_ref} codewords (kml_ref_frames)",
+                "reference": f"tests/golden/bench/{fn} (oracle/_ref: the reference's own sources, SourceSink::CntErr)",
+                "ref_err_bit": ref_bit, "ref_err_blk": ref_blk,
+                "gpu_err_bit": int(gc["err_bit"]), "gpu_err_blk": int(gc["err_blk"]),
+                "per_codeword_equal": same,
+                "exact": same and ref_bit == int(gc["err_bit"]) and ref_blk == int(gc["err_blk"]),
+            },
+        })
     line = {
         "metric": "decoded codewords/sec (N=2304 R=1/2, 20 BP iters) at 1/2/4/8 GPUs; BER match",
         "value": round(value, 1),
@@ -251,11 +432,20 @@ def main():
             "global_batch": B * world,
             "parallelism": f"codeword-sharded x{world}",
         },
+        "dist_backend": args.dist_backend if world > 1 else None,
+        "rccl_ranks": ranks_seen if (world > 1 and args.dist_backend == "nccl") else (1 if world == 1 else None),
+        "ranks": ranks_seen,
+        "rank_ms_per_step": [round(t / args.steps * 1e3, 3) for t in per_rank],
+        "full_loop": {
+            "value": round(fl_n * B * world / fl_max, 1) if fl_max > 0 else None,
+            "unit": "codewords/s",
+            "batches": fl_n,
+            "what": "kml_sim_generate (Philox source + encoder + channel) + receive, fresh frames per batch",
+        },
         "roofline": {
-            # The decoder keeps every message in LDS, so it is bound by the fp64
-            # pipes, not HBM: "mfma" here is the fp64 compute roof (MI355X fp64
-            # dense peak; no matrix instructions are used).
-            "bound": "mfma",
+            # Messages are LDS-resident; the kernel is bound by the fp64 vector
+            # pipes (no matrix instructions): the roof is MI355X's fp64 peak.
+            "bound": "fp64-valu",
             "achieved": round(achieved_tf, 2),
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",
@@ -266,29 +456,28 @@ def main():
             "alg_flops_per_launch": round(bp_flops),
             "alg_flops_rule": "per executed VN phase sum_cols (68*d-23), per CN phase sum_rows (73*d-52) fp64 flops "
                               "(DESIGN.md: Roofline); known-channel QPSK launches also run the demap in their "
-                              "prologue, whose work is not counted (conservative)",
+                              "prologue, whose work is not counted",
+            "frac_executed": frac_exec,
             "issue_view": issue_view,
+            "pmc": pmc_note,
             "hbm_view": {
-                "alg_bytes_per_launch": round(bp_bytes),
-                "achieved_GBs": round(achieved_gbs, 1),
+                "counter_bytes_per_launch": traffic,
+                "counter_GBs": round(traffic / (bp_avg_ms * 1e-3) / 1e9, 1) if traffic and bp_avg_ms > 0 else None,
                 "peak_GBs": HBM_PEAK_GBS,
-                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                "rule": "SURVEY 8(d) flooding-schedule bytes: VN phase 24E+9N, CN phase 24E, + 8*cc_len P0 per "
-                        "codeword; >1 means the LDS-resident decoder beats the flooding HBM roofline",
+                "frac": round(traffic / (bp_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                if traffic and bp_avg_ms > 0 else None,
+                "flooding_model_bytes_per_launch": round(bp_bytes),
+                "bytes_avoided_vs_flooding_model": round(bp_bytes - traffic) if traffic else None,
+                "rule": "counter bytes = (2*FETCH_SIZE + WRITE_SIZE) per launch (gfx950 correction, "
+                        "MI355X_MICROARCH.md); the flooding model (SURVEY 8d: VN 24E+9N, CN 24E bytes per phase) "
+                        "is what an HBM-resident decoder would move; LDS residency avoids it",
             },
         },
-        "stats": {
-            "fer": err_blk / max(tot_blk, 1),
-            "ber": err_bit / max(tot_bit, 1),
-            "mean_cn_phases": cn / max(tot_blk, 1),
-            "mean_vn_phases": vn / max(tot_blk, 1),
-            "stage_ms_per_step": {s: round(v["ms"] / max(args.steps, 1), 4) for s, v in stages.items() if v["launches"]},
-            "bp_ms_per_step": round(bp["ms"] / max(args.steps, 1), 4),
-        },
+        "stats": stats,
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(d, args)
-    print(json.dumps(line))
+    print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

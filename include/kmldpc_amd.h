@@ -195,6 +195,12 @@ int kml_sweep_point(const kml_point_cfg *cfg, kml_batch_fn decode, void *decode_
  * [histogram] enable from the config). */
 int kml_sim_point(kml_ctx *ctx, const kml_point_cfg *cfg, uint64_t seed, kml_allreduce_fn reduce, void *reduce_user,
                   kml_report_fn report, void *report_user, uint64_t *counters);
+/* Load B host frames (uu[B][K] source-bit bytes, y[B][S][2], true h[B][2])
+ * into the resident batch in place of kml_sim_generate, e.g. the reference's
+ * own seed-17 stream from kml_ref_frames, so kml_sim_decode's counters can be
+ * compared with SourceSink::CntErr's (sourcesink.cc:29-47) on identical frames. */
+int kml_sim_load(kml_ctx *ctx, double snr, const uint8_t *uu, const double *y, const double *h, int B,
+                 uint64_t first_cw);
 /* Copy the resident frames out (for checks): uu[B][K] bytes, y[B][S][2], h[B][2]. */
 int kml_sim_frames(kml_ctx *ctx, uint8_t *uu, double *y, double *h);
 

@@ -85,6 +85,7 @@ def lib():
         "kml_sim_decode": (I, [P, D, I, P, I]),
         "kml_sync": (I, [P]),
         "kml_sim_frames": (I, [P, P, P, P]),
+        "kml_sim_load": (I, [P, D, P, P, P, I, C.c_uint64]),
         "kml_prof_enable": (I, [P, I]),
         "kml_prof_reset": (I, [P]),
         "kml_prof_read": (I, [P, C.c_char_p, P, P, P]),
@@ -312,6 +313,15 @@ class Context:
         self._chk(lib().kml_sim_point(self._h, C.byref(cfg), int(seed), rf, None, pf, None, _p(cnt)),
                   "kml_sim_point")
         return dict(zip(["err_bit", "err_blk", "tot_bit", "tot_blk"], [int(x) for x in cnt]))
+
+    def sim_load(self, snr, uu, y, h, first_cw=0):
+        """Make host frames (uu[B][K] bytes, y[B][S][2], true h[B][2]) the resident batch (kml_sim_load)."""
+        uu = np.ascontiguousarray(uu, np.uint8).reshape(-1, self.K)
+        B = uu.shape[0]
+        y = _f64(y, (B, self.S, 2))
+        h = _f64(h, (B, 2))
+        self._chk(lib().kml_sim_load(self._h, float(snr), _p(uu), _p(y), _p(h), B, int(first_cw)), "kml_sim_load")
+        self._sim_B = B
 
     def sim_frames(self, B):
         uu = np.zeros((B, self.K), np.uint8)

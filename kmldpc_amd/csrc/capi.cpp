@@ -1193,6 +1193,33 @@ int kml_sync(kml_ctx *c) {
   return sync(c);
 }
 
+int kml_sim_load(kml_ctx *c, double snr, const uint8_t *uu, const double *y, const double *h, int B,
+                 uint64_t first_cw) {
+  if (!c || B < 0 || (B > 0 && (!uu || !y || !h))) return fail(c, KML_E_ARG, "kml_sim_load: bad argument");
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const kml::LdpcCode &L = c->code;
+  const int S = L.cc_len / c->modem.bits;
+  HIPCHK(c, c->s_uu.ensure(sizeof(uint64_t) * (size_t)std::max(B, 1) * L.Kw), "hipMalloc(sim uu)");
+  HIPCHK(c, c->s_y.ensure(sizeof(double2) * (size_t)std::max(B, 1) * S), "hipMalloc(sim y)");
+  HIPCHK(c, c->s_h.ensure(sizeof(double2) * (size_t)std::max(B, 1)), "hipMalloc(sim h)");
+  TRY(sync(c));
+  // source bits packed as the frame generator writes them: bit i of word i/64
+  std::vector<uint64_t> w((size_t)B * L.Kw, 0);
+  for (int b = 0; b < B; b++)
+    for (int i = 0; i < L.K; i++)
+      if (uu[(size_t)b * L.K + i]) w[(size_t)b * L.Kw + (i >> 6)] |= 1ull << (i & 63);
+  if (B > 0) {
+    HIPCHK(c, hipMemcpy(c->s_uu.p, w.data(), w.size() * 8, hipMemcpyHostToDevice), "H2D");
+    HIPCHK(c, hipMemcpy(c->s_y.p, y, sizeof(double2) * (size_t)B * S, hipMemcpyHostToDevice), "H2D");
+    HIPCHK(c, hipMemcpy(c->s_h.p, h, sizeof(double2) * (size_t)B, hipMemcpyHostToDevice), "H2D");
+  }
+  c->sim_B = B;
+  c->sim_snr = snr;
+  c->sim_first = first_cw;
+  return KML_OK;
+}
+
 int kml_sim_frames(kml_ctx *c, uint8_t *uu, double *y, double *h) {
   if (!c) return KML_E_ARG;
   TRY(need_gpu(c));

@@ -134,6 +134,8 @@ def main(argv=None):
     ap.add_argument("config", nargs="?", default="config.toml")
     ap.add_argument("--batch", type=int, default=int(os.environ.get("KML_BATCH", "32768")))
     ap.add_argument("--seed", type=int, default=int(os.environ.get("KML_SEED", "0")))
+    ap.add_argument("--dist-backend", default=os.environ.get("KML_DIST_BACKEND", "nccl"),
+                    help="nccl (RCCL over xGMI, one GPU per rank) or gloo (CPU counters; ranks may share a GPU)")
     args = ap.parse_args(argv)
     t0 = time.monotonic()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -150,8 +152,12 @@ def main(argv=None):
     if world > 1:
         import torch
         import torch.distributed as dist_mod
-        torch.cuda.set_device(local)
-        dist_mod.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist_mod.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            local = local % max(torch.cuda.device_count(), 1)
+            dist_mod.init_process_group(backend="gloo")
         dist = dist_mod
     sim = Simulator(args.config, device=local, batch=args.batch, seed=args.seed, dist=dist, log=log)
     sim.Simulate()

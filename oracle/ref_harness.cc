@@ -147,6 +147,7 @@ int main(int argc, char **argv) {
     lab::SourceSink ssink;
     ssink.ClrCnt();
     std::vector<int> uu(K), cc(N), uu_hat(K);
+    std::vector<int32_t> cw_errs;  // per-codeword error bits (for the BER sigma)
     for (int i = 0; i < ncw; i++) {
       ssink.GetBitStr(uu.data(), K);
       codec.Encoder(uu.data(), cc.data());
@@ -170,6 +171,9 @@ int main(int argc, char **argv) {
       }
       codec.Decoder(mls, h_hats, uu_hat.data());
       ssink.CntErr(uu.data(), uu_hat.data(), K, 1);
+      int e = 0;
+      for (int k = 0; k < K; k++) e += uu[k] != uu_hat[k];
+      cw_errs.push_back(e);
     }
     put_i32(f, (int32_t)ssink.tot_blk());
     put_i32(f, (int32_t)ssink.err_blk());
@@ -177,6 +181,7 @@ int main(int argc, char **argv) {
     double ber = ssink.ber();
     put_f64(f, ber);
     put_f64(f, ssink.fer());
+    for (int32_t e : cw_errs) put_i32(f, e);
     fclose(f);
     return 0;
   }

@@ -3,7 +3,10 @@
 TEST INFRASTRUCTURE ONLY.  Run in the build container (needs /root/reference and
 oracle/_ref/ref_harness, built by ``make -C oracle ref``):
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py                 # data files, CASES, counters.json
+    python tests/golden/make_golden.py --cases a,b     # regenerate the named CASES only
+    python tests/golden/make_golden.py --sweep         # sweep/cfg5.npz (PEG8064 blind sweep counters)
+    python tests/golden/make_golden.py --bench         # bench/*.npz (bench workload's reference counters)
 
 What it writes (all small):
   tests/golden/data/*.txt.gz      the reference's H-matrix and constellation data
@@ -64,6 +67,24 @@ SOFT_CASES = {
     "peg2304_qpsk_softhist": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 3.0, 300, 5, "softhist"),
     "bg2_16qam_soft": ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, False, 50, 5.01, 100, 5, "soft"),
     "peg2304_16qam_soft_it3": ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", False, False, 20, 7.0, 150, 3, "soft"),
+}
+
+# cfg5 (BASELINE.json configs[4]): the PEG8064 + 64QAM-Gray blind Eb/N0 0..4 dB
+# sweep, snr = Eb/N0 + 10*log10(R*m) = Eb/N0 + 4.77 (6.77 is peg8064_64qam_blind).
+SWEEP_SNRS = [4.77, 5.77, 6.77, 7.77, 8.77]
+for _snr in SWEEP_SNRS:
+    if _snr != 6.77:
+        CASES[f"peg8064_64qam_blind_s{int(round(_snr * 100))}"] = (
+            "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, False, 20, _snr, 24, True)
+NVEC_CASE = {k: 2 for k in CASES if k.startswith("peg8064_64qam_blind_s")}
+SWEEP_N = 400
+
+# the bench workload's reference counters: the first B codewords of the seed-17
+# stream through the reference itself (SourceSink::CntErr), with per-codeword
+# error bits for the BER standard error; tests/golden/bench/<name>.npz
+BENCH_CASES = {
+    "peg2304_qpsk_known_32768": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, True, 20, 2.0, 32768, True),
+    "peg2304_qpsk_blind_32768": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.0, 32768, True),
 }
 
 COUNTER_CASES = {
@@ -219,7 +240,117 @@ def make_rng(tmp, n=2000):
     print("rng:", {k: v[:3] for k, v in arr.items()})
 
 
+def run_simulate(tmp, name, mat, mod, is5g, known, it, snr, n, active=True):
+    """Harness 'simulate' mode: the reference's counters plus per-codeword error bits."""
+    cfg = os.path.join(tmp, name + ".toml")
+    write_toml(cfg, REF_CFG, mat, mod, is5g, known, it, active)
+    out = os.path.join(tmp, name + ".bin")
+    subprocess.run([HARNESS, cfg, repr(snr), str(n), out, "simulate"], check=True)
+    buf = open(out, "rb").read()
+    K = struct.unpack_from("<i", buf, 4)[0]
+    Kc = struct.unpack_from("<i", buf, 4 * 5)[0]
+    r = Reader(buf)
+    r.o = 4 * 10 + 8 + 16 * Kc
+    tot_blk, err_blk = r.i32(), r.i32()
+    ber, fer = r.f64(), r.f64()
+    errs = np.frombuffer(buf, dtype="<i4", count=n, offset=r.o).copy()
+    assert r.o + 4 * n == len(buf) and tot_blk == n
+    assert int((errs > 0).sum()) == err_blk and abs(errs.sum() / (K * n) - ber) < 1e-15
+    return dict(K=K, tot_blk=tot_blk, err_blk=err_blk, err_bit=int(errs.sum()), ber=ber, fer=fer), errs
+
+
+def make_frames_cases(tmp, names):
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(name):
+        mat, mod, is5g, known, it, snr, n, active = CASES[name]
+        cfg = os.path.join(tmp, name + ".toml")
+        write_toml(cfg, REF_CFG, mat, mod, is5g, known, it, active)
+        out = os.path.join(tmp, name + ".bin")
+        subprocess.run([HARNESS, cfg, repr(snr), str(n), out], check=True)
+        hdr, cons, recs = parse_frames(open(out, "rb").read())
+        arrs = {
+            "hdr_json": np.frombuffer(json.dumps(dict(hdr, matrix=mat, modem=mod, active=active)).encode(), dtype=np.uint8),
+            "cons": cons,
+            "s_chosen": np.array([d["chosen"] for d in recs], np.int32),
+            "s_ret": np.array([d["ret"] for d in recs], np.int32),
+            "s_errs": np.array([d["errs"] for d in recs], np.int32),
+            "s_crc_y": np.array([crc(d["y"]) for d in recs], np.uint32),
+            "s_crc_p0": np.array([crc(d["p0"]) for d in recs], np.uint32),
+            "s_crc_uuhat": np.array([crc(d["uu_hat"]) for d in recs], np.uint32),
+            "s_crc_cchat": np.array([crc(d["cc_hat"]) for d in recs], np.uint32),
+            "s_crc_syn": np.array([crc(d["syn"]) for d in recs], np.uint32),
+            "s_crc_uu": np.array([crc(d["uu"]) for d in recs], np.uint32),
+            "s_hhat": np.array([d["h_hat"] for d in recs]),
+            "s_metrics": np.array([d["metrics"] for d in recs]),
+            "s_true_h": np.array([d["true_h"] for d in recs]),
+        }
+        nv = min(NVEC_CASE.get(name, NVEC), len(recs))
+        for key in ["uu", "cc", "y", "p0", "cc_hat", "syn", "uu_hat"]:
+            arrs["v_" + key] = np.stack([recs[i][key] for i in range(nv)])
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+        return f"{name}: n={n} FER={np.mean(arrs['s_errs'] > 0):.4f} mean_ret={arrs['s_ret'].mean():.2f}"
+
+    with ThreadPoolExecutor(4) as ex:
+        for line in ex.map(one, names):
+            print(line)
+
+
+def make_sweep(tmp):
+    """cfg5 sweep: the reference's counters over SWEEP_N codewords per point ->
+    tests/golden/sweep/cfg5.npz (snr[P], counters[P][4], errs[P][SWEEP_N])."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(snr):
+        return run_simulate(tmp, f"sweep_{snr}", "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, False, 20,
+                            snr, SWEEP_N)
+
+    with ThreadPoolExecutor(5) as ex:
+        res = list(ex.map(one, SWEEP_SNRS))
+    cnt = np.array([[c["err_bit"], c["err_blk"], c["K"] * c["tot_blk"], c["tot_blk"]] for c, _ in res], np.int64)
+    os.makedirs(os.path.join(HERE, "sweep"), exist_ok=True)
+    np.savez_compressed(os.path.join(HERE, "sweep", "cfg5.npz"), snr=np.array(SWEEP_SNRS), counters=cnt,
+                        errs=np.stack([e for _, e in res]).astype(np.int16))
+    for snr, (c, _) in zip(SWEEP_SNRS, res):
+        print(f"cfg5 snr {snr}: FER {c['fer']:.4f} BER {c['ber']:.6f}")
+
+
+def make_bench(tmp):
+    from concurrent.futures import ThreadPoolExecutor
+
+    os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
+
+    def one(name):
+        mat, mod, is5g, known, it, snr, n, active = BENCH_CASES[name]
+        c, errs = run_simulate(tmp, name, mat, mod, is5g, known, it, snr, n, active)
+        hdr = dict(c, matrix=mat, modem=mod, is5g=is5g, known=known, max_iter=it, snr=snr, n=n, seed=17)
+        np.savez_compressed(os.path.join(HERE, "bench", name + ".npz"),
+                            hdr_json=np.frombuffer(json.dumps(hdr).encode(), dtype=np.uint8),
+                            errs=errs.astype(np.int16))
+        return f"{name}: FER {c['fer']:.5f} BER {c['ber']:.6f}"
+
+    with ThreadPoolExecutor(2) as ex:
+        for line in ex.map(one, BENCH_CASES):
+            print(line)
+
+
 def main():
+    for flag, fn in (("--bench", make_bench), ("--sweep", make_sweep)):
+        if flag in sys.argv:
+            tmp = tempfile.mkdtemp()
+            try:
+                fn(tmp)
+            finally:
+                shutil.rmtree(tmp)
+            return
+    if "--cases" in sys.argv:
+        names = sys.argv[sys.argv.index("--cases") + 1].split(",")
+        tmp = tempfile.mkdtemp()
+        try:
+            make_frames_cases(tmp, names)
+        finally:
+            shutil.rmtree(tmp)
+        return
     if "--rng" in sys.argv:
         tmp = tempfile.mkdtemp()
         try:

@@ -1,0 +1,220 @@
+"""GPU tests of the measurement path (SURVEY §8 rows d/e, a13, cfg5):
+
+* the sim path's CntErr (the BP epilogue's packed-bit error count,
+  bp_common.hpp) against an independent count of uu_hat != uu for every
+  codeword, on all three kernel families;
+* the bench's BER match: the reference's own seed-17 stream decoded through
+  the resident-batch path reproduces the reference's per-codeword error bits
+  (tests/golden/bench, made by oracle/_ref = the reference's sources);
+* Monte-Carlo BER of GPU (Philox) frames within 1 sigma of the reference BER;
+* `bench.py --gpus 2` really runs 2 ranks (gloo here, RCCL on a multi-GPU node)
+  and sums their counters;
+* cfg5: the PEG8064 + 64QAM-Gray blind Eb/N0 0..4 dB sweep through the
+  simulator driver, sharded over 2 ranks, equals the 1-rank run and matches
+  the reference's sweep counters statistically.
+"""
+import json
+import math
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REPO, write_config
+
+import kmldpc_amd as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(data_dir, tmp_path, matrix, modem, is5g=False, known=True, max_iter=20, snr=2.0, **kw):
+    cfg = str(tmp_path / f"c_{matrix}_{known}.toml")
+    write_config(cfg, data_dir, matrix, modem, is5g=is5g, known=known, max_iter=max_iter, snr=snr, **kw)
+    return K.Context(cfg, data_dir=data_dir, device=0)
+
+
+def _bench_fixture(name):
+    z = np.load(os.path.join(GOLDEN, "bench", name + ".npz"))
+    return json.loads(bytes(z["hdr_json"]).decode()), z["errs"].astype(np.int64)
+
+
+def _ber_sigma(errs, Kb):
+    e = np.asarray(errs, np.float64)
+    return e.std(ddof=1) / math.sqrt(len(e)) / Kb
+
+
+# (matrix, modem, is5g, max_iter, snr, known, B): one per kernel family, plus blind
+SIM_CASES = [
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, 20, 2.0, True, 4096),      # bp_regular_kernel (fused demap)
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, 20, 2.0, False, 2048),     # blind: k-means + metric + BP
+    ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, 50, 5.01, True, 2048),  # bp_irregular_kernel
+    ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 20, 6.77, True, 512),    # bp_part_kernel
+]
+
+
+@pytest.mark.parametrize("matrix,modem,is5g,max_iter,snr,known,B", SIM_CASES)
+def test_sim_cnterr_matches_independent_count(data_dir, tmp_path, matrix, modem, is5g, max_iter, snr, known, B):
+    """kml_sim_decode_ex's per-codeword error bits (the BP epilogue's
+    ballot/popcount CntErr) equal (uu_hat != uu).sum() with uu_hat from
+    kml_decode_frames on the same frames and uu from the frame generator."""
+    ctx = _ctx(data_dir, tmp_path, matrix, modem, is5g=is5g, known=known, max_iter=max_iter, snr=snr)
+    ctx.sim_generate(snr, B, seed=123, first_cw=5000)
+    uu, y, h = ctx.sim_frames(B)
+    cw_err, _, c = ctx.sim_decode_ex(snr, blind=not known)
+    r = ctx.decode_frames(y, snr, h if known else None)
+    indep = (r["uu_hat"] != uu).sum(axis=1)
+    assert np.array_equal(cw_err, indep)
+    assert c["err_bit"] == int(indep.sum()) and c["err_blk"] == int((indep > 0).sum())
+    assert c["tot_blk"] == B and c["tot_bit"] == B * ctx.K
+    assert 0 < c["err_blk"] < B or snr > 6  # a non-trivial mix of right and wrong codewords
+    ctx.close()
+
+
+@pytest.mark.parametrize("name,n", [("peg2304_qpsk_known_32768", 32768), ("peg2304_qpsk_blind_32768", 8192)])
+def test_bench_reference_stream_is_exact(data_dir, tmp_path, name, n):
+    """The bench's ber_match leg: the first n codewords of the reference's
+    seed-17 stream loaded as the resident batch (kml_sim_load) give, codeword by
+    codeword, the error bits the reference's SourceSink::CntErr counted."""
+    hdr, ref = _bench_fixture(name)
+    ctx = _ctx(data_dir, tmp_path, hdr["matrix"], hdr["modem"], known=hdr["known"], max_iter=hdr["max_iter"],
+               snr=hdr["snr"])
+    uu, th, y = ctx.ref_frames(K.CLCRandNum(hdr["seed"]), hdr["snr"], n)
+    ctx.sim_load(hdr["snr"], uu, y, th)
+    cw_err, _, c = ctx.sim_decode_ex(hdr["snr"], blind=not hdr["known"])
+    assert np.array_equal(cw_err, ref[:n])
+    assert c["err_bit"] == int(ref[:n].sum()) and c["err_blk"] == int((ref[:n] > 0).sum())
+    if n == hdr["n"]:
+        assert (c["err_bit"], c["err_blk"]) == (hdr["err_bit"], hdr["err_blk"])
+    ctx.close()
+
+
+@pytest.mark.parametrize("name,B,seed", [("peg2304_qpsk_known_32768", 65536, 11),
+                                         ("peg2304_qpsk_blind_32768", 32768, 12)])
+def test_gpu_monte_carlo_ber_within_1sigma(data_dir, tmp_path, name, B, seed):
+    """north_star: BER within 1 sigma of the reference.  GPU (Philox) frames
+    vs the reference's 32768-codeword seed-17 run of the same point; sigma
+    combines both standard errors (codeword = unit, since bit errors within a
+    codeword are dependent).  FER is checked at 2 sigma (binomial)."""
+    hdr, ref = _bench_fixture(name)
+    Kb = hdr["K"]
+    ctx = _ctx(data_dir, tmp_path, hdr["matrix"], hdr["modem"], known=hdr["known"], max_iter=hdr["max_iter"],
+               snr=hdr["snr"])
+    ctx.sim_generate(hdr["snr"], B, seed=seed)
+    cw_err, _, c = ctx.sim_decode_ex(hdr["snr"], blind=not hdr["known"])
+    ber, ber_ref = c["err_bit"] / c["tot_bit"], ref.sum() / (len(ref) * Kb)
+    sig = math.hypot(_ber_sigma(cw_err, Kb), _ber_sigma(ref, Kb))
+    fer, fer_ref = c["err_blk"] / B, float(np.mean(ref > 0))
+    fsig = math.sqrt(fer_ref * (1 - fer_ref) * (1 / B + 1 / len(ref)))
+    print(f"{name}: GPU BER {ber:.6f} vs reference {ber_ref:.6f}, sigma {sig:.6f}, z {(ber - ber_ref) / sig:+.3f}; "
+          f"FER {fer:.5f} vs {fer_ref:.5f} (sigma {fsig:.5f})")
+    assert abs(ber - ber_ref) <= sig
+    assert abs(fer - fer_ref) <= 2 * fsig
+    ctx.close()
+
+
+def _bench(args, timeout=300):
+    env = dict(os.environ, PYTHONPATH=REPO)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_gloo(data_dir, tmp_path):
+    """`bench.py --gpus 2` launches 2 rank processes itself (torch.distributed.run
+    as a child), both decode their shard of global codeword indices, and the
+    counters of rank 0's line are the sum over both shards — equal to one
+    decode of the whole index range."""
+    B = 2048
+    line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--steps", "2", "--warmup", "1", "--batch", str(B),
+                   "--no-cpu-baseline", "--no-ber-match", "--full-loop-batches", "1"])
+    assert line["n_gpus"] == 2 and line["ranks"] == 2 and line["dist_backend"] == "gloo"
+    assert len(line["rank_ms_per_step"]) == 2 and line["config"]["global_batch"] == 2 * B
+    st = line["stats"]
+    assert st["codewords"] == 2 * B
+    ctx = _ctx(data_dir, tmp_path, "PEG2304regular0.5.txt", "2bits_QPSK.txt")
+    ctx.sim_generate(2.0, 2 * B, seed=17, first_cw=0)
+    c = ctx.sim_decode(2.0, blind=False)
+    assert round(st["fer"] * 2 * B) == c["err_blk"]
+    assert round(st["ber"] * c["tot_bit"]) == c["err_bit"]
+    assert line["full_loop"]["value"] > 0 and line["value"] > 0
+    ctx.close()
+
+
+def test_bench_single_rank_line(data_dir):
+    """The N=1 line carries the roofline (fp64-valu), the exact BER match on
+    the reference stream and the 1-sigma statistic."""
+    line = _bench(["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--full-loop-batches", "1"])
+    assert line["n_gpus"] == 1 and line["rccl_ranks"] == 1
+    rf = line["roofline"]
+    assert rf["bound"] == "fp64-valu" and 0 < rf["frac"] < 1
+    bm = line["stats"]["ber_match"]
+    assert bm["exact"] and bm["per_codeword_equal"]
+    assert isinstance(line["stats"]["ber_within_1sigma"], bool)
+
+
+CFG5_SNRS = [4.77, 5.77, 6.77, 7.77, 8.77]
+_PAT = re.compile(r"^(\d\.\d{3}) (\d\.\d{14})$")
+
+
+def _tables(out):
+    """The BER / FER result tables of the driver's console output."""
+    msgs = [ln.split("[INFO]\x1b[0m ", 1)[1] for ln in out.splitlines() if "[INFO]" in ln]
+    i, j = msgs.index("BER Result"), msgs.index("FER Result")
+    ber = {m.group(1): float(m.group(2)) for m in map(_PAT.match, msgs[i + 1:j]) if m}
+    fer = {m.group(1): float(m.group(2)) for m in map(_PAT.match, msgs[j + 1:j + 1 + len(ber)]) if m}
+    return ber, fer
+
+
+def test_cfg5_sweep_sharded_matches_single_rank_and_reference(data_dir, tmp_path):
+    """cfg5 (BASELINE configs[4]): PEG8064 + 64QAM-Gray, blind k-means, Eb/N0
+    0..4 dB (snr 4.77..8.77), through the simulator driver
+    (Simulator::Simulate, simulator.cc:25-67).  Two ranks sharing this GPU
+    (gloo counters) print the same BER/FER tables as one rank — codeword
+    indices, not ranks, key the frames — and every point's BER lies within
+    3 sigma of the reference's own 400-codeword counters (golden/sweep/cfg5.npz);
+    the bit-exact parity of the same points is test_decode_frames_vs_reference_stream
+    on the peg8064_64qam_blind_s* fixtures."""
+    z = np.load(os.path.join(GOLDEN, "sweep", "cfg5.npz"))
+    assert list(np.round(z["snr"], 2)) == CFG5_SNRS
+    cfg = tmp_path / "config.toml"
+    nblk = 1536
+    write_config(str(cfg), data_dir, "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", known=False, snr=4.77,
+                 snr_max=8.77, snr_step=1.0, max_blocks=nblk, max_err=10 ** 9, thread_blocks=nblk)
+    env = dict(os.environ, PYTHONPATH=REPO, KML_BATCH="384", KML_SEED="7", KML_DIST_BACKEND="gloo",
+               OMP_NUM_THREADS="1")
+    r1 = subprocess.run([sys.executable, "-m", "kmldpc_amd.simulate", str(cfg)], cwd=tmp_path, env=env,
+                        capture_output=True, text=True, timeout=300)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    r2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                         "--master-addr=127.0.0.1", "--master-port=29533", "-m", "kmldpc_amd.simulate", str(cfg)],
+                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    b1, f1 = _tables(r1.stdout)
+    b2, f2 = _tables(r2.stdout)
+    assert b1 == b2 and f1 == f2 and len(b1) == 5
+    from kmldpc_amd.simulate import point_seed
+    ctx = _ctx(data_dir, tmp_path, "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", known=False, snr=4.77)
+    Kb = ctx.K
+    for p, snr in enumerate(CFG5_SNRS):
+        key = f"{snr:.3f}"
+        # the driver's frames of this point, decoded directly: same counters, plus the per-codeword spread
+        s = 4.77 + 1.0 * p
+        ctx.sim_generate(s, nblk, seed=point_seed(7, p), first_cw=0)
+        cw_err, _, c = ctx.sim_decode_ex(s, blind=True)
+        assert abs(b1[key] - c["err_bit"] / c["tot_bit"]) < 1e-13 and abs(f1[key] - c["err_blk"] / nblk) < 1e-13
+        ref = z["errs"][p].astype(np.float64)
+        ber_ref = ref.sum() / (len(ref) * Kb)
+        sig = math.hypot(_ber_sigma(ref, Kb), _ber_sigma(cw_err, Kb))
+        z_p = (b1[key] - ber_ref) / sig
+        print(f"cfg5 snr {snr}: GPU BER {b1[key]:.6f} FER {f1[key]:.4f} vs reference BER {ber_ref:.6f} "
+              f"FER {np.mean(ref > 0):.4f} (sigma {sig:.6f}, z {z_p:+.2f})")
+        assert abs(z_p) <= 3, snr
+    ctx.close()
+    bers = [b1[f"{s:.3f}"] for s in CFG5_SNRS]
+    assert all(a >= b for a, b in zip(bers, bers[1:]))  # BER falls with SNR

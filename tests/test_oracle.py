@@ -192,3 +192,50 @@ def test_soft_metric_stream_matches_reference(case, data_dir):
             assert np.array_equal(met, z["metrics"][i]), (case, i)
         else:  # parsed from the codec's "%.14f" log records
             assert np.allclose(met, z["metrics"][i], rtol=0, atol=6e-15 * np.maximum(1, np.abs(met))), (case, i)
+
+
+# --- the bench workload's and cfg5's reference counters (tests/golden/bench, sweep)
+
+def _oracle_errs(data_dir, matrix, modem, is5g, known, max_iter, snr, n):
+    code = O.Code(os.path.join(data_dir, matrix), bool(is5g), True, False, max_iter)
+    md = O.Modem(os.path.join(data_dir, modem))
+    uu, _, th, y = O.gen_frames(code, md, snr, n)
+    syn = np.zeros(code.M)
+    out = []
+    for i in range(n):
+        r = O.receive(code, md, y[i], th[i], snr, not known, syn=syn)
+        out.append(int(np.sum(r["uu_hat"] != uu[i].astype(np.uint8))))
+    return np.array(out)
+
+
+@pytest.mark.parametrize("name,n", [("peg2304_qpsk_known_32768", 300), ("peg2304_qpsk_blind_32768", 120)])
+def test_oracle_reproduces_bench_fixture(name, n, data_dir):
+    """The bench's BER-match reference (the reference's own SourceSink counters
+    over the first 32768 seed-17 codewords): self-consistent, and its first n
+    per-codeword error counts are reproduced by the oracle."""
+    z = np.load(os.path.join(GOLDEN, "bench", name + ".npz"))
+    hdr = json.loads(bytes(z["hdr_json"]).decode())
+    errs = z["errs"].astype(np.int64)
+    assert len(errs) == hdr["n"] == hdr["tot_blk"]
+    assert int(errs.sum()) == hdr["err_bit"] and int((errs > 0).sum()) == hdr["err_blk"]
+    assert abs(hdr["ber"] - hdr["err_bit"] / (hdr["K"] * hdr["n"])) < 1e-15
+    got = _oracle_errs(data_dir, hdr["matrix"], hdr["modem"], hdr["is5g"], hdr["known"], hdr["max_iter"], hdr["snr"],
+                       n)
+    assert np.array_equal(got, errs[:n])
+    # the 2000-codeword counters of counters.json are a prefix of this stream
+    ctr = json.load(open(os.path.join(GOLDEN, "counters.json")))
+    c2k = ctr["peg2304_qpsk_known_2000" if hdr["known"] else "peg2304_qpsk_blind_2000"]
+    assert int(errs[:2000].sum()) == c2k["err_bit"] and int((errs[:2000] > 0).sum()) == c2k["err_blk"]
+
+
+def test_oracle_reproduces_cfg5_sweep_fixture(data_dir):
+    """cfg5 sweep counters (PEG8064 + 64QAM-Gray blind, snr 4.77..8.77, the
+    reference's simulate mode): the oracle reproduces each point's first
+    codewords of the seed-17 stream."""
+    z = np.load(os.path.join(GOLDEN, "sweep", "cfg5.npz"))
+    assert z["errs"].shape == (5, 400)
+    for p, snr in enumerate(z["snr"]):
+        e = z["errs"][p].astype(np.int64)
+        assert int(e.sum()) == z["counters"][p][0] and int((e > 0).sum()) == z["counters"][p][1]
+        got = _oracle_errs(data_dir, "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, False, 20, float(snr), 6)
+        assert np.array_equal(got, e[:6]), snr
