@@ -19,6 +19,8 @@
  *                             + h_hat = clusters[0]/c[0] and its 4 rotations       src/simulator.cc:145-148
  *   kml_decode_frames         void KmCodec::Decoder(ModemLinearSystem&, const std::vector<complex>& h_hats, int *uu_hat)
  *                                                                                  include/kmcodec.h:23-25
+ *   kml_decode_candidates     the same KmCodec::Decoder with the caller's h_hats (any 1..4 estimates)
+ *                                                                                  include/kmcodec.h:23-25
  *   kml_count_errors          void SourceSink::CntErr(const int*, const int*, int, int)  lib/lab/include/sourcesink.h:15
  *   kml_sim_*                 the throughput driver: frame generation + receive + counting for one
  *                             SNR point of Simulator::run_blocks (src/simulator.cc:112-168)
@@ -128,6 +130,16 @@ int kml_kmeans(kml_ctx *ctx, const double *y, int B, int iters, double *h_hat, d
  * chosen[B], metrics[B][4], ret[B], h_hat[B][2]. */
 int kml_decode_frames(kml_ctx *ctx, const double *y, const double *true_h, double snr, int B, uint8_t *uu_hat,
                       int32_t *chosen, double *metrics, int32_t *ret, double *h_hat, int flags);
+
+/* KmCodec::Decoder(mls, h_hats, uu_hat) (include/kmcodec.h:23-25,
+ * src/kmcodec.cc:54-72) with the caller's channel estimates h_hats[B][nc][2],
+ * 1 <= nc <= 4: nc == 1 demaps with h_hats[b][0] and decodes (no metric);
+ * nc > 1 computes every candidate's syndrome metric (hard PEG count, 5G
+ * metric_iter BP count, or the soft metric, as configured), takes the first
+ * minimum, demaps with it and decodes.  chosen[B], metrics[B][4] (entries
+ * >= nc are 0), ret[B] may be NULL.  KML_HISTOGRAM: metrics only. */
+int kml_decode_candidates(kml_ctx *ctx, const double *y, const double *h_hats, int nc, double snr, int B,
+                          uint8_t *uu_hat, int32_t *chosen, double *metrics, int32_t *ret, int flags);
 
 /* SourceSink::CntErr over B codewords; counters[4] += {err_bit, err_blk, tot_bit, tot_blk}. */
 int kml_count_errors(kml_ctx *ctx, const uint8_t *uu, const uint8_t *uu_hat, int B, uint64_t *counters, int flags);

@@ -81,6 +81,7 @@ def lib():
         "kml_kmeans": (I, [P, P, I, I, P, P, I]),
         "kml_decode_frames": (I, [P, P, P, D, I, P, P, P, P, P, I]),
         "kml_count_errors": (I, [P, P, P, I, P, I]),
+        "kml_decode_candidates": (I, [P, P, P, I, D, I, P, P, P, P, I]),
         "kml_sim_generate": (I, [P, D, C.c_uint64, C.c_uint64, I]),
         "kml_sim_decode": (I, [P, D, I, P, I]),
         "kml_sync": (I, [P]),
@@ -256,6 +257,20 @@ class Context:
         self._chk(lib().kml_decode_frames(self._h, _p(y), _p(th), float(snr), B, _p(uh), _p(ch), _p(met), _p(ret),
                                           _p(hh), KML_HISTOGRAM if histogram else 0), "kml_decode_frames")
         return dict(uu_hat=uh, chosen=ch, metrics=met, ret=ret, h_hat=hh)
+
+    def decode_candidates(self, y, h_hats, snr, histogram=False):
+        """KmCodec::Decoder with explicit estimates h_hats[B][nc][2] (kml_decode_candidates)."""
+        y = _f64(y, (-1, self.S, 2))
+        B = y.shape[0]
+        hh = _f64(h_hats, (B, -1, 2))
+        nc = hh.shape[1]
+        uh = np.zeros((B, self.K), np.uint8)
+        ch = np.zeros(B, np.int32)
+        met = np.zeros((B, 4))
+        ret = np.zeros(B, np.int32)
+        self._chk(lib().kml_decode_candidates(self._h, _p(y), _p(hh), nc, float(snr), B, _p(uh), _p(ch), _p(met),
+                                              _p(ret), KML_HISTOGRAM if histogram else 0), "kml_decode_candidates")
+        return dict(uu_hat=uh, chosen=ch, metrics=met, ret=ret)
 
     def count_errors(self, uu, uu_hat):
         uu = np.ascontiguousarray(uu, np.uint8).reshape(-1, self.K)

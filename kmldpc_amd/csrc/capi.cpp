@@ -94,6 +94,7 @@ struct kml_ctx {
   double soft_state = -INFINITY;
   // resident simulation frames
   DBuf s_uu, s_cc, s_y, s_h;
+  DBuf w_hc;  // caller candidates (kml_decode_candidates)
   int sim_B = 0;
   double sim_snr = 0;
   uint64_t sim_first = 0;
@@ -447,6 +448,8 @@ int need_gpu(kml_ctx *c) {
 struct RecvIO {
   const double2 *y = nullptr;
   const double2 *true_h = nullptr;  // known channel (simulator.cc:132-133); NULL = blind
+  const double2 *cand = nullptr;    // caller's candidates [B][ncand] (KmCodec::Decoder h_hats), ncand > 1
+  int ncand = 0;
   uint8_t *uh = nullptr;            // uu_hat[B][K] (NULL: not kept)
   int32_t *chosen = nullptr;        // [B]
   double *met = nullptr;            // [B][4]
@@ -509,7 +512,10 @@ int receive(kml_ctx *c, const RecvIO &io, double snr, int B, int &bp_slot) {
   // k-means + 4 rotations (simulator.cc:136-148)
   const double2 *hc;
   int nc;
-  if (io.true_h) {
+  if (io.cand) {
+    hc = io.cand;
+    nc = io.ncand;
+  } else if (io.true_h) {
     hc = io.true_h;
     nc = 1;
   } else {
@@ -853,7 +859,7 @@ void kml_destroy(kml_ctx *c) {
     drain_profile(c);
     for (DBuf *b : {&c->d_graph, &c->d_cons, &c->d_arena, &c->d_queue, &c->d_gslots, &c->d_gsync, &c->d_gcch, &c->w_y, &c->w_h, &c->w_h4,
                     &c->w_hhat, &c->w_p0, &c->w_uu, &c->w_uh, &c->w_uh4, &c->w_cwerr, &c->w_ret, &c->w_cch, &c->w_syn, &c->w_sel, &c->w_met,
-                    &c->w_pc, &c->w_cnt, &c->w_km, &c->s_synm, &c->s_synf, &c->s_itm, &c->s_itf, &c->s_Lm, &c->s_Lf, &c->s_list, &c->s_sel, &c->s_uu, &c->s_cc, &c->s_y, &c->s_h})
+                    &c->w_pc, &c->w_cnt, &c->w_km, &c->s_synm, &c->s_synf, &c->s_itm, &c->s_itf, &c->s_Lm, &c->s_Lf, &c->s_list, &c->s_sel, &c->s_uu, &c->s_cc, &c->s_y, &c->s_h, &c->w_hc})
       b->release();
     hipStreamDestroy(c->stream);
   }
@@ -1041,6 +1047,48 @@ int kml_decode_frames(kml_ctx *c, const double *y, const double *true_h, double 
   }
   TRY(copy_out(c, uu_hat, d_uh, (size_t)B * c->code.K, flags));
   if (io.histogram) {  // no final decode: no BP return value
+    if (ret && !(flags & KML_DEVICE_PTRS)) memset(ret, 0, sizeof(int32_t) * B);
+  } else {
+    TRY(copy_out(c, ret, d_ret, (size_t)B, flags));
+  }
+  return sync(c);
+}
+
+int kml_decode_candidates(kml_ctx *c, const double *y, const double *h_hats, int nc, double snr, int B,
+                          uint8_t *uu_hat, int32_t *chosen, double *metrics, int32_t *ret, int flags) {
+  if (!c || !y || !h_hats || !uu_hat || B < 0 || nc < 1 || nc > 4)
+    return fail(c, KML_E_ARG, "kml_decode_candidates: bad argument (need 1 <= nc <= 4)");
+  if (nc == 1)  // one estimate: no metric (kmcodec.cc:66-67)
+    return kml_decode_frames(c, y, h_hats, snr, B, uu_hat, chosen, metrics, ret, nullptr, flags & ~KML_HISTOGRAM);
+  if (B == 0) return KML_OK;
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const int S = c->code.cc_len / c->modem.bits;
+  const double *d_y, *d_hc;
+  TRY(stage_in(c, c->w_y, y, (size_t)B * S * 2, flags, d_y));
+  TRY(stage_in(c, c->w_hc, h_hats, (size_t)B * nc * 2, flags, d_hc));
+  uint8_t *d_uh;
+  int32_t *d_ch, *d_ret;
+  double *d_met;
+  TRY(stage_out_ptr(c, c->w_uh, uu_hat, (size_t)B * c->code.K, flags, d_uh));
+  TRY(stage_out_ptr(c, c->w_sel, chosen, (size_t)B, flags, d_ch));
+  TRY(stage_out_ptr(c, c->w_met, metrics, (size_t)B * 4, flags, d_met));
+  TRY(stage_out_ptr(c, c->w_ret, ret, (size_t)B, flags, d_ret));
+  int slot;
+  RecvIO io;
+  io.y = reinterpret_cast<const double2 *>(d_y);
+  io.cand = reinterpret_cast<const double2 *>(d_hc);
+  io.ncand = nc;
+  io.uh = d_uh;
+  io.chosen = d_ch;
+  io.met = d_met;
+  io.ret = d_ret;
+  io.histogram = (flags & KML_HISTOGRAM) != 0;
+  TRY(receive(c, io, snr, B, slot));
+  TRY(copy_out(c, chosen, d_ch, (size_t)B, flags));
+  TRY(copy_out(c, metrics, d_met, (size_t)B * 4, flags));
+  TRY(copy_out(c, uu_hat, d_uh, (size_t)B * c->code.K, flags));
+  if (io.histogram) {
     if (ret && !(flags & KML_DEVICE_PTRS)) memset(ret, 0, sizeof(int32_t) * B);
   } else {
     TRY(copy_out(c, ret, d_ret, (size_t)B, flags));

@@ -31,6 +31,7 @@ typedef struct {
   int32_t *uu;
   double *y, *h;
   long err_bits, err_blk;
+  double sum_e2;
   double syn_dummy;
 } job;
 
@@ -63,6 +64,7 @@ static void *dec(void *p) {
   double *syn = (double *)calloc(M, sizeof(double));
   j->err_bits = 0;
   j->err_blk = 0;
+  j->sum_e2 = 0;
   for (int i = 0; i < j->n; i++) {
     orc_receive(j->c, j->m, j->y + (size_t)i * 2 * S, j->h + 2 * i, j->snr, j->blind, 0, 5, uh, NULL, NULL, NULL,
                 NULL, NULL, syn);
@@ -71,6 +73,7 @@ static void *dec(void *p) {
     for (int t = 0; t < K; t++) e += (u[t] != uh[t]);
     j->err_bits += e;
     j->err_blk += (e > 0);
+    j->sum_e2 += (double)e * e;
   }
   free(uh);
   free(syn);
@@ -119,13 +122,16 @@ int main(int argc, char **argv) {
   for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
   double el = now() - t0;
   long eb = 0, ek = 0;
+  double e2 = 0;
   for (int t = 0; t < T; t++) {
     eb += jobs[t].err_bits;
     ek += jobs[t].err_blk;
+    e2 += jobs[t].sum_e2;
   }
   long tot = (long)n * T;
   printf("{\"codewords\": %ld, \"threads\": %d, \"seconds\": %.6f, \"cw_per_s\": %.3f, \"gen_seconds\": %.6f, "
-         "\"full_loop_cw_per_s\": %.3f, \"err_blk\": %ld, \"err_bit\": %ld, \"fer\": %.6f, \"ber\": %.8f}\n",
-         tot, T, el, tot / el, gen_s, tot / (el + gen_s), ek, eb, (double)ek / tot, (double)eb / ((double)tot * K));
+         "\"full_loop_cw_per_s\": %.3f, \"err_blk\": %ld, \"err_bit\": %ld, \"sum_e2\": %.1f, \"K\": %d, "
+         "\"fer\": %.6f, \"ber\": %.8f}\n",
+         tot, T, el, tot / el, gen_s, tot / (el + gen_s), ek, eb, e2, K, (double)ek / tot, (double)eb / ((double)tot * K));
   return 0;
 }

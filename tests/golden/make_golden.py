@@ -7,6 +7,7 @@ oracle/_ref/ref_harness, built by ``make -C oracle ref``):
     python tests/golden/make_golden.py --cases a,b     # regenerate the named CASES only
     python tests/golden/make_golden.py --sweep         # sweep/cfg5.npz (PEG8064 blind sweep counters)
     python tests/golden/make_golden.py --bench         # bench/*.npz (bench workload's reference counters)
+    python tests/golden/make_golden.py --bench-large   # bench/large_oracle.json (oracle, 8 streams)
 
 What it writes (all small):
   tests/golden/data/*.txt.gz      the reference's H-matrix and constellation data
@@ -334,8 +335,37 @@ def make_bench(tmp):
             print(line)
 
 
+# Larger reference samples of the bench points for the Monte-Carlo BER sigma:
+# the oracle restatement (bit-exact vs the reference, tests/test_oracle.py) on
+# 8 Park-Miller streams (seeds 17..24), n_per_stream codewords each.
+BENCH_LARGE = {
+    "peg2304_qpsk_known": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, True, 20, 2.0, 32768),
+    "peg2304_qpsk_blind": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.0, 16384),
+}
+
+
+def make_bench_large(tmp):
+    exe = os.path.join(REPO, "oracle", "cpu_baseline")
+    for fn in DATA_FILES:
+        with open(os.path.join(REF_CFG, fn), "rb") as f, open(os.path.join(tmp, fn), "wb") as g:
+            g.write(f.read())
+    out = {}
+    for name, (mat, mod, is5g, known, it, snr, n) in BENCH_LARGE.items():
+        r = subprocess.run([exe, os.path.join(tmp, mat), os.path.join(tmp, mod), str(int(is5g)), repr(snr), str(it),
+                            str(int(not known)), str(n), "8"], check=True, capture_output=True, text=True)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        out[name] = dict(matrix=mat, modem=mod, is5g=is5g, known=known, max_iter=it, snr=snr, streams=8,
+                         seeds="17..24", codewords=d["codewords"], err_bit=d["err_bit"], err_blk=d["err_blk"],
+                         sum_e2=d["sum_e2"], K=d["K"], ber=d["ber"], fer=d["fer"],
+                         source="oracle/cpu_baseline (oracle.c restatement, bit-exact vs the reference)")
+        print(name, out[name])
+    os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
+    with open(os.path.join(HERE, "bench", "large_oracle.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def main():
-    for flag, fn in (("--bench", make_bench), ("--sweep", make_sweep)):
+    for flag, fn in (("--bench", make_bench), ("--sweep", make_sweep), ("--bench-large", make_bench_large)):
         if flag in sys.argv:
             tmp = tempfile.mkdtemp()
             try:

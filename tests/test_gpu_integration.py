@@ -1,0 +1,38 @@
+"""The reference-side shims on the GPU, against the reference's own CPU
+classes in the same process (oracle/_ref/shim_check: the reference's sources
+compiled in the build container + integration/kmldpc_gpu_codecs.hpp + the
+product library).  Every codeword of the reference's seed-17 stream goes
+through lab::BinaryLDPCCodec::Decoder and GpuBinaryLDPCCodec::Decoder,
+KmCodec::Decoder and GpuKmCodec::Decoder, the reference KMeans and
+gpu_kmeans_h_hats: no mismatch is allowed in any output."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from conftest import REPO, write_config
+
+pytestmark = pytest.mark.gpu
+EXE = os.path.join(REPO, "oracle", "_ref", "shim_check")
+
+
+@pytest.mark.skipif(not os.path.exists(EXE), reason="oracle/_ref/shim_check not built (needs /root/reference)")
+@pytest.mark.parametrize("matrix,modem,is5g,known,max_iter,snr,n", [
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, True, 20, 2.0, 200),
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.0, 100),
+    ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, True, 50, 5.01, 40),
+    ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, False, 50, 5.01, 30),
+])
+def test_reference_side_shims_match_reference_classes(data_dir, tmp_path, matrix, modem, is5g, known, max_iter, snr, n):
+    cfg = str(tmp_path / "config.toml")
+    write_config(cfg, data_dir, matrix, modem, is5g=is5g, known=known, max_iter=max_iter, snr=snr)
+    r = subprocess.run([EXE, cfg, repr(snr), str(n)], capture_output=True, text=True, timeout=240, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    print(res)
+    assert res["codewords"] == n
+    for k in ("kmcodec_uu_mismatch", "candidate_mismatch", "bp_ret_mismatch", "bp_uu_mismatch", "bp_cc_hat_mismatch",
+              "bp_syndrom_soft_mismatch"):
+        assert res[k] == 0, k
+    assert res["err_bit_ref"] == res["err_bit_gpu"] and res["err_bit_ref"] > 0
