@@ -473,6 +473,10 @@ def main():
             "traffic": traffic,
             "kernel": f"{bp_kernel} ({KERNEL_NOTES.get(bp_kernel, 'sum-product BP')})",
             "avg_launch_ms": round(bp_avg_ms, 4),
+            # ordinal range of this kernel's dispatches inside the timed region
+            # (tools/trace_window.py reads it against a rocprofv3 kernel trace)
+            "timed_dispatches": {"kernel": bp_kernel.split()[0], "count": int(bp["launches"]),
+                                 "first": int(bp["launches"]) // max(args.steps, 1) * args.warmup},
             "alg_flops_per_launch": round(bp_flops),
             "alg_flops_rule": "per executed VN phase sum_cols (68*d-23), per CN phase sum_rows (73*d-52) fp64 flops "
                               "(DESIGN.md: Roofline); known-channel QPSK launches also run the demap in their "

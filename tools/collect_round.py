@@ -25,11 +25,24 @@ def main():
             f.write(line + "\n")
     shutil.copy(os.path.join(SRC, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{pre}_kernel_stats.csv"))
     shutil.copy(os.path.join(SRC, "gpu_tests.log"), os.path.join(dst, f"{pre}_gpu_tests.log"))
+    # the timed-window average of the traced bench command (what avg_launch_ms describes)
+    subprocess.run([sys.executable, os.path.join(REPO, "tools", "trace_window.py"),
+                    os.path.join(SRC, "trace", "run_kernel_trace.csv"), os.path.join(SRC, "trace_bench.json"),
+                    "--out", os.path.join(dst, f"{pre}_bp_timed_window.json")], check=True, capture_output=True)
+    shutil.copy(os.path.join(SRC, "trace_bench.json"), os.path.join(dst, f"{pre}_trace_bench.json"))
     dirs = [os.path.join(SRC, d) for d in ["pmc_fetch", "pmc_write", "pmc_a", "pmc_b", "pmc_c"]]
     out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), *dirs, "--kernel",
                           "bp_regular_kernel"], capture_output=True, text=True, check=True).stdout
     with open(os.path.join(dst, f"{pre}_pmc_bp.txt"), "w") as f:
         f.write(out)
+    # the summary bench.py reads (headline kernel/workload, this source tree's src_sha)
+    sys.path.insert(0, REPO)
+    import bench
+
+    subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), *dirs, "--kernel",
+                    "bp_regular_kernel", "--json", os.path.join(dst, "pmc_bp.json"), "--batch", "32768",
+                    "--workload", "PEG2304regular0.5.txt", "--waves-per-simd", "3", "--round", pre,
+                    "--src-sha", bench.src_sha()], capture_output=True, text=True, check=True)
     print("wrote", pre, "evidence to profiles/")
 
 

@@ -10,7 +10,7 @@ mkdir -p $O
 cd $R
 step() { echo "== $1 $(date +%T)" >> $O/steps.log; }
 step tests
-timeout -k 10 700 python -m pytest tests -m gpu -q > $O/gpu_tests.log 2>&1 || exit $?
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit $?
 step bench
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit $?
 step bench_blind

@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--workload")
     ap.add_argument("--alg-bytes-per-launch", type=float)
     ap.add_argument("--waves-per-simd", type=float, help="resident waves per SIMD of the kernel (issue view)")
+    ap.add_argument("--round", help="evidence label (e.g. r02_v1)")
+    ap.add_argument("--src-sha", help="bench.src_sha() of the kernel sources the counters were taken at")
     args = ap.parse_args()
     rows = []
     for d in args.dirs:
@@ -66,6 +68,15 @@ def main():
         if fetch is not None and write is not None:
             out["hbm_bytes_per_launch"] = (2 * fetch + write) * 1024
             out["hbm_bytes_per_launch_uncorrected"] = (fetch + write) * 1024
+        if args.round:
+            out["round"] = args.round
+        if args.src_sha:
+            out["src_sha"] = args.src_sha
+        flops = res.get("SQ_INSTS_VALU_FLOPS_FP64", (None, 0))[0]
+        if flops:
+            # per-wave flop count (FMA 2, add/mul/trans 1) x 64 lanes: every lane of
+            # the BP kernels' waves is active in the fp64 phases
+            out["fp64_flops_executed_per_launch"] = 64 * flops
         if args.alg_bytes_per_launch:
             out["alg_bytes_per_launch"] = args.alg_bytes_per_launch
         # VALU issue view: every wave64 VALU instruction holds a SIMD for 4
