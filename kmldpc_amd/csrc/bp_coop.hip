@@ -55,6 +55,9 @@ struct GroupSync {
   // partitioned kernel: barrier counters by barrier parity, arrivals in the
   // low 32 bits, parity-failure reports in the high 32 bits (part_barrier)
   unsigned long long bar2[2];
+  // tagged exchange: early-stop flags per iteration parity and member,
+  // ((global iteration + 1) << 1) | (the member has failing rows)
+  unsigned long long mflag[2][4];
 };
 
 constexpr int kPartG = 4;  // workgroups per codeword of the partitioned kernel
@@ -66,6 +69,13 @@ size_t part_lds_bytes(const DevCode &c) {
 }
 
 constexpr long long kSpinLimit = 20000000;  // ~1 s of s_sleep(1) polls
+
+// The tagged mailboxes (bp_part_kernel) follow the barrier-exchange ones in
+// the group's E double2 of scratch: 3 ncut doubles, rounded to 16 bytes, then
+// another 3 ncut.
+__host__ __device__ constexpr bool part_tagged_fits(int E, int ncut) { return 6LL * ncut + 2 <= 2LL * E; }
+// byte offset of the deferred-codeword count in the sync block (past the abort word)
+constexpr size_t part_defer_offset(int groups) { return sizeof(GroupSync) * (size_t)groups + 16; }
 
 __device__ __forceinline__ unsigned ld_rlx(const unsigned *p) {  // L1-bypassing (sc1) load
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -562,13 +572,18 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
                                                 unsigned long long *bst, unsigned &nb, int *sfail, bool same_xcd,
                                                 unsigned *abort, unsigned char *smem,
                                                 uint8_t *dec, double2 *mb_v2c, double *mb_c2v, uint8_t *gc,
-                                                const int (&vaddr)[RV][3], const int (&vpos)[RV],
+                                                const DevCode &c, const int (&vaddr)[RV][3], const int (&vpos)[RV],
                                                 const bool (&vact)[RV], const double (&pv)[RV], const int (&crow)[RC],
-                                                const int (&cbase)[RC], const int (&ccol)[RC][3],
+                                                const int (&cbase)[RC],
                                                 const bool (&cact)[RC], const int (&xr)[RX], const int (&xc)[RX],
                                                 int odd, int member, int &iter_out, bool &conv_out) {
   constexpr int DV = 3, DC = 6, H = 3;
   const int tid = threadIdx.x;
+  int ccol[RC][H];  // parity-check columns (positions in dec): even lane edges [0, H), odd lane [H, DC)
+#pragma unroll
+  for (int r = 0; r < RC; ++r)
+#pragma unroll
+    for (int k = 0; k < H; ++k) ccol[r][k] = c.pt_pos[c.row_col[c.row_ptr[crow[r]] + (odd ? H + k : k)]];
   double2 *slots = reinterpret_cast<double2 *>(smem);
   int iter = 0;
   bool conv = false;
@@ -592,7 +607,7 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
 #pragma unroll
       for (int r = 0; r < RV; ++r)
 #pragma unroll
-        for (int k = 0; k < DV; ++k) c0s[r][k] = *reinterpret_cast<const double *>(smem + vaddr[r][k]);
+        for (int k = 0; k < DV; ++k) c0s[r][k] = *reinterpret_cast<const double *>(smem + (vaddr[r][k] & 0xFFFF) * 16);
       double a0[RV], a1[RV], al0[RV][DV], al1[RV][DV];
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
@@ -636,7 +651,7 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
             div2<FAST, true>(t0, t1, t0 + t1, q0, q1);
           else
             div2<FAST>(t0, t1, t0 + t1, q0, q1);
-          if (vact[r]) *reinterpret_cast<double2 *>(smem + vaddr[r][k]) = make_double2(q0, q1);
+          if (vact[r]) *reinterpret_cast<double2 *>(smem + (vaddr[r][k] & 0xFFFF) * 16) = make_double2(q0, q1);
           if (k > 0) {
             const double c0 = c0s[r][k];
             if (unit) {  // the sum rounds to exactly 1 (bp_common.hpp)
@@ -766,11 +781,344 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
   return true;
 }
 
+// ---------------------------------------------------------------------------
+// Tagged exchange (FAST codewords of same-XCD groups): no group barrier inside
+// the iterations.  Every cut edge has one mailbox entry per direction, and
+// the entry's producer writes it directly from the arithmetic (plain store,
+// landing in the XCD's L2) with a TAG in the sign bit of every word: the
+// parity of the group's global iteration counter g (all members run the same
+// iterations, so they agree on g).  A consumer polls its entries (L1-bypassing
+// loads) until the tags read g & 1.  FAST messages lie in [0, 1], so bits 63
+// and 62 of their words are zero; the v2c entry also carries the column's
+// hard decision in bit 62 of its first word, which replaces the exchange of
+// the decision array for the row owner's parity check.
+// Why one tag bit is enough: each entry is written exactly once per global
+// iteration (the CN phase runs speculatively in the converged iteration too),
+// and its producer cannot write it again before the consumer has read it:
+// v2c(e) of iteration g+1 follows the VN phase that polled c2v(e) of iteration
+// g, which the row owner computes only after its CN lanes polled v2c(e) of
+// iteration g (every lane polls all its entries before any arithmetic); the
+// symmetric argument holds for c2v, and across codewords the early-stop flags
+// of iteration g (posted after the member's loads of iteration g) gate the
+// next codeword's first writes.
+// Early stop: after its CN phase every member posts (g + 1, failing rows?) to
+// its flag word of parity g & 1, and wave 0 polls the members' flags (one per
+// lane) after its c2v receive.  A flag word is rewritten (iteration g + 2)
+// only after every member passed iteration g + 1's closing barrier, which
+// follows its poll of the iteration-g flags.  (Per-wave flags posted without
+// the CN-closing barrier measured slower: 9.30 vs 8.71 ms per 4096 cw.)
+constexpr unsigned kTagHi = 0x80000000u;  // bit 63 of a message word (hi dword bit 31)
+constexpr unsigned kHdHi = 0x40000000u;   // bit 62: hard decision (v2c first word)
+
+__device__ __forceinline__ double or_hi(double x, unsigned bits) {
+  return __hiloint2double(__double2hiint(x) | (int)bits, __double2loint(x));
+}
+__device__ __forceinline__ double and_hi(double x, unsigned mask) {
+  return __hiloint2double(__double2hiint(x) & (int)mask, __double2loint(x));
+}
+__device__ __forceinline__ unsigned hi_of(unsigned long long w) { return (unsigned)(w >> 32); }
+
+// Mailbox accesses through a buffer resource (SGPRs) and 32-bit byte offsets:
+// no 64-bit per-lane addresses to keep live across the phases.  Polls load
+// with sc1 (L2-served, bypassing the never-refreshed vector L1).
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kBufFlags = 0x00020000;  // gfx9 raw buffer resource, dword 3
+constexpr int kAuxSc1 = 16;            // cache-policy operand: sc1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mailbox_rsrc(void *p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, bytes, kBufFlags);
+}
+__device__ __forceinline__ unsigned long long mb_ld64(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, kAuxSc1);
+  return ((unsigned long long)v.y << 32) | v.x;
+}
+__device__ __forceinline__ void mb_st64(__amdgpu_buffer_rsrc_t r, unsigned off, double x) {
+  const u32x2 v = {(unsigned)__double2loint(x), (unsigned)__double2hiint(x)};
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void mb_st128(__amdgpu_buffer_rsrc_t r, unsigned off, double x, double y) {
+  const u32x4 v = {(unsigned)__double2loint(x), (unsigned)__double2hiint(x), (unsigned)__double2loint(y),
+                   (unsigned)__double2hiint(y)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 0);
+}
+
+// Poll n (<= R) mailbox entries of W words (8 B each) until every word's tag
+// bit equals tag, then store them to LDS.  entry q = (x << 16) | LDS slot, or
+// < 0 when absent.  Returns false on a timeout / aborted launch.
+template <int R, int W>
+__device__ __forceinline__ bool poll_entries(const int (&ent)[R], __amdgpu_buffer_rsrc_t mb, unsigned mb_off,
+                                             unsigned char *smem, unsigned tag, unsigned *abort) {
+  bool need[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) need[q] = ent[q] >= 0;
+  for (long long spin = 0;; ++spin) {
+    unsigned long long w[R][W];
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+      if (need[q]) {
+#pragma unroll
+        for (int i = 0; i < W; ++i) w[q][i] = mb_ld64(mb, mb_off + (unsigned)(ent[q] >> 16) * (8 * W) + 8 * i);
+      }
+    bool pend = false;
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+      if (need[q]) {
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < W; ++i) ok = ok && (hi_of(w[q][i]) >> 31) == tag;
+        if (ok) {
+          // stored without the tags (a v2c message keeps its hard-decision bit)
+          unsigned long long *d = reinterpret_cast<unsigned long long *>(smem + (ent[q] & 0xFFFF) * 16);
+#pragma unroll
+          for (int i = 0; i < W; ++i) d[i] = w[q][i] & ~(1ull << 63);
+          need[q] = false;
+        } else {
+          pend = true;
+        }
+      }
+    if (!pend) return true;
+    if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
+      __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 template <int kG, int T, int RV, int RC, int RX, bool SYN>
+__device__ __forceinline__ bool part_iterations_tagged(
+    const BpLaunch &a, int M, int cw, GroupSync *gs, unsigned &g, int *sfail, int *sdead, int member,
+    unsigned *abort, unsigned char *smem, uint8_t *dec, __amdgpu_buffer_rsrc_t tb, unsigned tb_c2v,
+    const int (&vaddr)[RV][3],
+    const int (&vpos)[RV], const bool (&vact)[RV], const double (&pv)[RV], const int (&crow)[RC],
+    const int (&cbase)[RC], const int (&crx)[RC], const bool (&cact)[RC], const int (&xr)[RX], const int (&xc)[RX],
+    int odd, int &iter_out, bool &conv_out, int &pcnt_out) {
+  constexpr int DV = 3, DC = 6, H = 3;
+  const int tid = threadIdx.x;
+  int iter = 0, pcnt = 0;
+  bool conv = false;
+#ifdef KML_STAMPS
+  unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
+#endif
+  for (; iter < a.iter_count; ++iter, ++g) {
+    const unsigned tag = g & 1u;
+    KML_STAMP(0);
+    // ------------------------------------------------------------ VN phase
+    // (c2v of cut edges sit in the mirror slots, received at the end of the
+    // previous iteration; iteration 0 reads InitMsg's 0.5)
+    __builtin_amdgcn_s_setprio(3);
+    {
+      double c0s[RV][DV];
+#pragma unroll
+      for (int r = 0; r < RV; ++r)
+#pragma unroll
+        for (int k = 0; k < DV; ++k)
+          c0s[r][k] = *reinterpret_cast<const double *>(smem + (vaddr[r][k] & 0xFFFF) * 16);
+      double a0[RV], a1[RV], al0[RV][DV], al1[RV][DV];
+      unsigned hdb[RV];
+#pragma unroll
+      for (int r = 0; r < RV; ++r) {
+        a0[r] = pv[r];
+        a1[r] = 1.0 - pv[r];
+      }
+#pragma unroll
+      for (int k = 0; k < DV; ++k)
+#pragma unroll
+        for (int r = 0; r < RV; ++r) {
+          al0[r][k] = a0[r];
+          al1[r][k] = a1[r];
+          const double c0 = c0s[r][k];
+          const double n0 = a0[r] * c0;
+          const double n1 = a1[r] * (1.0 - c0);
+          if (k + 1 < DV) {
+            div2<true>(n0, n1, n0 + n1, a0[r], a1[r]);
+          } else {
+            const int hd = hard_decision<true>(n0, n1);
+            hdb[r] = hd ? kHdHi : 0u;
+            if (vact[r]) dec[vpos[r]] = (unsigned char)hd;
+          }
+        }
+      double b0[RV], b1[RV];
+#pragma unroll
+      for (int r = 0; r < RV; ++r) b0[r] = b1[r] = 1.0;
+      __builtin_amdgcn_s_setprio(2);
+#pragma unroll
+      for (int k = DV - 1; k >= 0; --k) {
+        if (k == DV - 2) __builtin_amdgcn_s_setprio(1);
+        if (k == DV - 3) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+        for (int r = 0; r < RV; ++r) {
+          const bool unit = k == DV - 1;
+          const double t0 = unit ? al0[r][k] : al0[r][k] * b0[r];
+          const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
+          double q0, q1;
+          if (unit)
+            div2<true, true>(t0, t1, t0 + t1, q0, q1);
+          else
+            div2<true>(t0, t1, t0 + t1, q0, q1);
+          if (vact[r]) {
+            const int x1 = vaddr[r][k] >> 16;  // mailbox index + 1 of a cut edge, 0 for a row slot
+            if (x1) {
+              const unsigned tb_tag = tag ? kTagHi : 0u;
+              mb_st128(tb, (unsigned)(x1 - 1) * 16, or_hi(q0, tb_tag | hdb[r]), or_hi(q1, tb_tag));
+            } else {
+              *reinterpret_cast<double2 *>(smem + (vaddr[r][k] & 0xFFFF) * 16) = make_double2(or_hi(q0, hdb[r]), q1);
+            }
+          }
+          if (k > 0) {
+            const double c0 = c0s[r][k];
+            if (unit) {
+              b0[r] = c0;
+              b1[r] = 1.0 - c0;
+            } else {
+              div2<true>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r]);
+            }
+          }
+        }
+      }
+    }
+    KML_STAMP(2);
+    // ------------------------------------------- receive v2c of the cut edges
+    if (!poll_entries<RX, 2>(xr, tb, 0u, smem, tag, abort)) *sdead = 1;
+    KML_STAMP(4);
+    __syncthreads();
+    KML_STAMP(5);
+    if (*sdead) return false;
+
+    // ------------------------------------------ CN phase (+ the parity check)
+    // bp_regular.hip's step order: every load of a step before its stores.
+    // A message's first word carries the column's hard decision in bit 62
+    // (the receive strips the mailbox tags).
+    double syn0[RC];
+    int par[RC];
+    {
+      double x0[RC][H], x1[RC][H];
+      double s0[RC], s1[RC];
+#pragma unroll
+      for (int r = 0; r < RC; ++r) {
+        s0[r] = 1.0;
+        s1[r] = 0.0;
+        par[r] = 0;
+      }
+      __builtin_amdgcn_s_setprio(2);
+#pragma unroll
+      for (int st = 0; st < DC; ++st) {
+        if (st == 2) __builtin_amdgcn_s_setprio(1);
+        if (st == 4) __builtin_amdgcn_s_setprio(0);
+        const bool advance = SYN || st + 1 < DC || st < H;
+        double m0[RC], m1[RC];
+        if (advance) {
+#pragma unroll
+          for (int r = 0; r < RC; ++r) {
+            const double2 m = *reinterpret_cast<const double2 *>(smem + cbase[r] + (odd ? DC - 1 - st : st) * 16);
+            if (st < H) par[r] ^= (__double2hiint(m.x) >> 30) & 1;
+            m0[r] = and_hi(m.x, ~kHdHi);
+            m1[r] = m.y;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < RC; ++r) {
+          if (st < H) {
+            x0[r][st] = s0[r];
+            x1[r][st] = s1[r];
+          } else {
+            const double y0 = swap_pair(s0[r]);
+            const double y1 = swap_pair(s1[r]);
+            const double o0 = x0[r][DC - 1 - st], o1 = x1[r][DC - 1 - st];
+            const bool unit = st == DC - 1;
+            const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
+            const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
+            const double q = clip_c2v<true>(div1<true, true>(t0, t0 + t1));
+            if (cact[r]) {
+              const int e = odd ? st : DC - 1 - st;  // the edge this c2v belongs to
+              const int mask = crx[r] & 0xFF;
+              if ((mask >> e) & 1) {
+                const int x = (crx[r] >> 8) + __popc(mask & ((1 << e) - 1));
+                mb_st64(tb, tb_c2v + (unsigned)x * 8, or_hi(q, tag ? kTagHi : 0u));
+              } else {
+                *reinterpret_cast<double *>(smem + cbase[r] + e * 16) = q;
+              }
+            }
+          }
+        }
+        if (st + 1 < DC || SYN) {
+#pragma unroll
+          for (int r = 0; r < RC; ++r) {
+            const bool unit = st == 0;
+            const double n0 = unit ? m0[r] : s0[r] * m0[r] + s1[r] * m1[r];
+            const double n1 = unit ? m1[r] : s0[r] * m1[r] + s1[r] * m0[r];
+            div2<true, true>(n0, n1, n0 + n1, s0[r], s1[r]);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RC; ++r) syn0[r] = s0[r];
+    }
+    // the row's parity: the even lane XORed edges 0..2, the odd lane 5..3
+    int fail = 0, nfail = 0;
+#pragma unroll
+    for (int r = 0; r < RC; ++r) {
+      const int full = par[r] ^ swap_pair_i(par[r]);
+      fail |= cact[r] ? full : 0;
+      nfail += (cact[r] && !odd) ? full : 0;
+    }
+    pcnt = nfail;  // unsatisfied checks of this iteration's hard decisions (final if the loop ends here)
+    if (__ballot(fail) != 0 && (tid & 63) == 0) atomicOr(sfail, 1);
+    KML_STAMP(6);
+    __syncthreads();
+    KML_STAMP(7);
+    // ------------- post this member's flag; receive c2v; read the others' flags
+    __shared__ int sany;
+    if (tid == 0) {
+      const unsigned long long mine = ((unsigned long long)(g + 1) << 1) | (unsigned long long)(*sfail != 0);
+      *sfail = 0;
+      __hip_atomic_store(&gs->mflag[g & 1][member], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (iter + 1 < a.iter_count)
+      if (!poll_entries<RX, 1>(xc, tb, tb_c2v, smem, tag, abort)) *sdead = 1;
+    if (tid < 64) {  // wave 0: lane m polls member m's flag
+      unsigned long long v = (unsigned long long)(g + 1) << 1;
+      if (tid < kG) {
+        for (long long spin = 0;; ++spin) {
+          v = ld_rlx64(&gs->mflag[g & 1][tid]);
+          if ((v >> 1) == (unsigned long long)(g + 1)) break;
+          if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
+            __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *sdead = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      const bool any = __ballot((v & 1) != 0) != 0;
+      if (tid == 0) sany = any ? 1 : 0;
+    }
+    __syncthreads();
+    KML_STAMP(8);
+    if (*sdead) return false;
+    if (!sany) {  // every row satisfied: stop before this CN phase
+      conv = true;
+      pcnt = 0;
+      ++g;
+      break;
+    }
+    if constexpr (SYN) {
+#pragma unroll
+      for (int r = 0; r < RC; ++r)
+        if (cact[r] && !odd) a.syn[(long long)cw * M + crow[r]] = syn0[r];  // alpha past the last edge (:274)
+    }
+  }
+  iter_out = iter;
+  conv_out = conv;
+  pcnt_out = pcnt;
+  return true;
+}
+
+template <int kG, int T, int RV, int RC, int RX, bool SYN, bool TAGGED>
 __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, GroupSync *gsync, uint8_t *gcch,
                                                     unsigned *abort, unsigned int *queue, int fast_allowed) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int DV = 3, DC = 6, H = 3;
+  constexpr int DV = 3, DC = 6;
   const int tid = threadIdx.x;
   const int odd = tid & 1;
   const int member = (blockIdx.x >> 3) % kG;
@@ -779,10 +1127,15 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
   const int MG = c.M / kG, NG = c.N / kG, EG = MG * DC;
   double2 *mb_v2c = a.gslots + (size_t)group * c.E;       // [ncut] double2
   double *mb_c2v = reinterpret_cast<double *>(mb_v2c + c.pt_ncut);  // [ncut] double
+  // tagged mailboxes, after the barrier-exchange ones (16-byte aligned; part_tagged_fits)
+  double2 *tb_v2c = reinterpret_cast<double2 *>(reinterpret_cast<double *>(mb_v2c) + ((3 * c.pt_ncut + 1) & ~1));
+  const __amdgpu_buffer_rsrc_t tb = mailbox_rsrc(tb_v2c, 24 * c.pt_ncut);  // v2c [ncut] x 16 B, then c2v [ncut] x 8 B
+  const unsigned tb_c2v = 16u * (unsigned)c.pt_ncut;
   uint8_t *gc = gcch + (size_t)group * c.N;
   const int nslots = EG + c.pt_mirror;
   uint8_t *dec = smem + (size_t)nslots * 16;  // N hard decisions, plan order
 
+  // vaddr: (mailbox index + 1 of a cut edge, 0 for a row slot) << 16 | LDS slot (row slot or mirror)
   int vaddr[RV][DV], vpos[RV];
   bool vact[RV];
 #pragma unroll
@@ -791,9 +1144,10 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     vact[r] = i < NG;
     vpos[r] = member * NG + (vact[r] ? i : 0);
 #pragma unroll
-    for (int k = 0; k < DV; ++k) vaddr[r][k] = c.pt_vaddr[vpos[r] * DV + k];
+    for (int k = 0; k < DV; ++k)
+      vaddr[r][k] = ((c.pt_vx[vpos[r] * DV + k] + 1) << 16) | (c.pt_vaddr[vpos[r] * DV + k] >> 4);
   }
-  int crow[RC], cbase[RC], ccol[RC][H];
+  int crow[RC], cbase[RC], crx[RC];
   bool cact[RC];
 #pragma unroll
   for (int r = 0; r < RC; ++r) {
@@ -803,8 +1157,7 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     const int row = c.pt_cn[member * MG + li];
     crow[r] = row;
     cbase[r] = li * DC * 16;
-#pragma unroll
-    for (int k = 0; k < H; ++k) ccol[r][k] = c.pt_pos[c.row_col[c.row_ptr[row] + (odd ? H + k : k)]];
+    crx[r] = c.pt_rx[member * MG + li];
   }
   int xr[RX], xc[RX];
   {
@@ -820,15 +1173,24 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
 
   __shared__ unsigned long long bst[4];  // part_barrier state (thread 0)
   __shared__ int sfail;                  // this member's early-stop flag (parity failures)
+  __shared__ int sdead;                  // a tagged-exchange poll timed out: every wave leaves
+  __shared__ int spcnt;                  // unsatisfied checks of the member's rows (tagged path)
   unsigned nb = 0;                       // barrier sequence number (uniform, same on every member)
+  unsigned g = 0;                        // global iteration counter of the tagged exchange (same on every member)
   if (tid == 0) {
     bst[0] = bst[1] = bst[2] = bst[3] = 0;
     sfail = 0;
+    sdead = 0;
     const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
     __hip_atomic_fetch_or(&gs->xcc, 1u << xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (part_barrier<kG>(gs, bst, nb, false, abort, nullptr) < 0) return;
   const bool same_xcd = __popc(ld_rlx(&gs->xcc)) == 1;
+  // TAGGED: this launch decodes the FAST codewords of same-XCD groups with the
+  // tagged exchange and defers every other codeword to a barrier-exchange
+  // launch that follows it (a.defer_*); that launch takes its entry count
+  // from the device (a.B_dev).
+  const int B = a.B_dev ? (int)*a.B_dev : a.B;
 
   for (;;) {
     if (member == 0 && tid == 0) {
@@ -837,9 +1199,10 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
       __hip_atomic_store(&gs->errs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&gs->pcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (tid == 0) spcnt = 0;
     if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;
     const int entry = (int)ld_rlx(&gs->cw);
-    if (entry >= a.B) break;
+    if (entry >= B) break;
     const int cw = a.cw_idx ? a.cw_idx[entry] : entry;
     const double *p0 = a.p0 + (long long)cw * a.p0_stride;
     if (a.p0_sel) p0 += (long long)a.p0_sel[cw] * a.p0_sel_stride;
@@ -857,66 +1220,101 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     if (__ballot(!ok) != 0 && (tid & 63) == 0)
       __hip_atomic_fetch_or(&gs->nofast, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;
-    const bool fast = fast_allowed && !ld_rlx(&gs->nofast);
+    const bool fast = (fast_allowed & 1) && !ld_rlx(&gs->nofast);
+    constexpr bool tagged = TAGGED;
 
-    int iter = 0;
+    int iter = 0, pcnt = 0;
     bool conv = false;
     bool alive;
-    if (fast)
+    if constexpr (TAGGED) {
+      if (!fast || !same_xcd) {  // to the barrier-exchange launch
+        if (member == 0 && tid == 0) a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = cw;
+        continue;
+      }
+      alive = part_iterations_tagged<kG, T, RV, RC, RX, SYN>(a, c.M, cw, gs, g, &sfail, &sdead, member, abort, smem, dec,
+                                                          tb, tb_c2v, vaddr, vpos, vact, pv, crow, cbase, crx,
+                                                          cact, xr, xc, odd, iter, conv, pcnt);
+    } else if (fast) {
       alive = part_iterations<kG, RV, RC, RX, SYN, true>(a, c.M, c.N, NG, cw, gs, bst, nb, &sfail, same_xcd, abort, smem, dec,
-                                                         mb_v2c, mb_c2v, gc, vaddr, vpos, vact, pv, crow, cbase, ccol,
+                                                         mb_v2c, mb_c2v, gc, c, vaddr, vpos, vact, pv, crow, cbase,
                                                          cact, xr, xc, odd, member, iter, conv);
-    else
+    } else {
       alive = part_iterations<kG, RV, RC, RX, SYN, false>(a, c.M, c.N, NG, cw, gs, bst, nb, &sfail, same_xcd, abort, smem, dec,
-                                                          mb_v2c, mb_c2v, gc, vaddr, vpos, vact, pv, crow, cbase,
-                                                          ccol, cact, xr, xc, odd, member, iter, conv);
+                                                          mb_v2c, mb_c2v, gc, c, vaddr, vpos, vact, pv, crow, cbase,
+                                                          cact, xr, xc, odd, member, iter, conv);
+    }
     if (!alive) return;
 
-    // ---- outputs: every member holds all hard decisions in LDS (dec) and
-    // writes its share; member 0 the scalars
+    // ---- outputs
     if (a.iter_count > 0) {
-      if (a.uu_hat) {
-        uint8_t *u = a.uu_hat + (long long)cw * c.K;
-        const int lo = (int)((long long)c.K * member / kG), hi = (int)((long long)c.K * (member + 1) / kG);
-        for (int i = lo + tid; i < hi; i += T) u[i] = dec[c.pt_pos[i + c.info_off]];
-      }
-      if (a.cc_hat) {
-        uint8_t *o = a.cc_hat + (long long)cw * c.N;
-        for (int v = member * NG + tid; v < (member + 1) * NG; v += T) o[c.pt_vn[v]] = dec[v];
-      }
-      if (a.parity_cnt) {
-        int cnt = 0;
-#pragma unroll
-        for (int r = 0; r < RC; ++r) {
-          int p = 0;
-#pragma unroll
-          for (int k = 0; k < H; ++k) p ^= dec[ccol[r][k]];
-          const int full = p ^ swap_pair_i(p);
-          if (!odd && cact[r]) cnt += full;
+      if constexpr (tagged) {
+        // a member holds the decisions of its own columns: it writes theirs
+        for (int p = member * NG + tid; p < (member + 1) * NG; p += T) {
+          const int col = c.pt_vn[p];
+          const int hd = dec[p];
+          if (a.cc_hat) a.cc_hat[(long long)cw * c.N + col] = (uint8_t)hd;
+          const int i = col - c.info_off;
+          if (i >= 0 && i < c.K) {
+            if (a.uu_hat) a.uu_hat[(long long)cw * c.K + i] = (uint8_t)hd;
+            if (a.ref_bits) {
+              const int rb = (int)((a.ref_bits[(long long)cw * c.Kw + (i >> 6)] >> (i & 63)) & 1ull);
+              if (rb != hd) atomicAdd(&spcnt, 1 << 16);  // error bits in the high half
+            }
+          }
         }
-        if (cnt) __hip_atomic_fetch_add(&gs->pcnt, (unsigned)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (a.ref_bits) {
-        const uint64_t *ref = a.ref_bits + (long long)cw * c.Kw;
-        const int lo = (int)((long long)c.Kw * member / kG), hi = (int)((long long)c.Kw * (member + 1) / kG);
-        int errs = 0;
-        for (int w = lo + tid; w < hi; w += T) {
-          uint64_t word = 0;
-          const int base = w * 64;
-          const int nb = min(64, c.K - base);
-          for (int j = 0; j < nb; ++j) word |= (uint64_t)dec[c.pt_pos[c.info_off + base + j]] << j;
-          errs += __popcll(word ^ ref[w]);
+        if (a.parity_cnt && pcnt) atomicAdd(&spcnt, pcnt);
+        __syncthreads();
+        if (tid == 0) {
+          const int v = spcnt;
+          if (v >> 16) __hip_atomic_fetch_add(&gs->errs, (unsigned)(v >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (v & 0xFFFF)
+            __hip_atomic_fetch_add(&gs->pcnt, (unsigned)(v & 0xFFFF), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (errs) __hip_atomic_fetch_add(&gs->errs, (unsigned)errs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        // every member holds all hard decisions in LDS (dec) and writes its share
+        if (a.uu_hat) {
+          uint8_t *u = a.uu_hat + (long long)cw * c.K;
+          const int lo = (int)((long long)c.K * member / kG), hi = (int)((long long)c.K * (member + 1) / kG);
+          for (int i = lo + tid; i < hi; i += T) u[i] = dec[c.pt_pos[i + c.info_off]];
+        }
+        if (a.cc_hat) {
+          uint8_t *o = a.cc_hat + (long long)cw * c.N;
+          for (int v = member * NG + tid; v < (member + 1) * NG; v += T) o[c.pt_vn[v]] = dec[v];
+        }
+        if (a.parity_cnt) {
+          int cnt = 0;
+#pragma unroll
+          for (int r = 0; r < RC; ++r) {
+            int p = 0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) p ^= dec[c.pt_pos[c.row_col[c.row_ptr[crow[r]] + (odd ? 3 + k : k)]]];
+            const int full = p ^ swap_pair_i(p);
+            if (!odd && cact[r]) cnt += full;
+          }
+          if (cnt) __hip_atomic_fetch_add(&gs->pcnt, (unsigned)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (a.ref_bits) {
+          const uint64_t *ref = a.ref_bits + (long long)cw * c.Kw;
+          const int lo = (int)((long long)c.Kw * member / kG), hi = (int)((long long)c.Kw * (member + 1) / kG);
+          int errs = 0;
+          for (int w = lo + tid; w < hi; w += T) {
+            uint64_t word = 0;
+            const int base = w * 64;
+            const int nbits = min(64, c.K - base);
+            for (int j = 0; j < nbits; ++j) word |= (uint64_t)dec[c.pt_pos[c.info_off + base + j]] << j;
+            errs += __popcll(word ^ ref[w]);
+          }
+          if (errs) __hip_atomic_fetch_add(&gs->errs, (unsigned)errs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
     if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;  // the members' sums are complete
     if (member == 0 && tid == 0) {
       const int errs = (int)ld_rlx(&gs->errs);
-      const int pcnt = (int)ld_rlx(&gs->pcnt);
+      const int pc = (int)ld_rlx(&gs->pcnt);
       if (a.ret) a.ret[cw] = iter + (iter < a.max_iter);
       if (a.iters) a.iters[cw] = iter;
-      if (a.parity_cnt) a.parity_cnt[cw] = a.iter_count > 0 ? pcnt : 0;
+      if (a.parity_cnt) a.parity_cnt[cw] = a.iter_count > 0 ? pc : 0;
       if (a.cw_err && a.ref_bits) a.cw_err[cw] = a.iter_count > 0 ? errs : 0;
       if (a.counters) {
         const unsigned long long vn = conv ? (unsigned long long)iter + 1 : (unsigned long long)iter;
@@ -934,23 +1332,28 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
   }
 }
 
-template <int kG, int T, int RV, int RC, int RX, bool SYN>
-hipError_t launch_part_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast, int groups) {
-  auto kern = bp_part_kernel<kG, T, RV, RC, RX, SYN>;
+template <int kG, int T, int RV, int RC, int RX, bool SYN, bool TAGGED>
+hipError_t launch_part_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast, int groups, bool reset_abort) {
+  auto kern = bp_part_kernel<kG, T, RV, RC, RX, SYN, TAGGED>;
   const size_t lds = part_lds_bytes(c);
   hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(a.queue, 0, sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(a.gsync, 0, sizeof(GroupSync) * (size_t)groups + sizeof(unsigned), s);
+  // the group blocks, and the abort word unless this launch follows one whose abort must persist
+  e = hipMemsetAsync(a.gsync, 0, sizeof(GroupSync) * (size_t)groups + (reset_abort ? sizeof(unsigned) : 0), s);
   if (e != hipSuccess) return e;
+  if (TAGGED) {  // every tagged mailbox word starts with tag 1 (the first iteration writes tag 0)
+    e = hipMemsetAsync(a.gslots, 0xFF, sizeof(double2) * (size_t)groups * c.E, s);
+    if (e != hipSuccess) return e;
+  }
   DevCode cc = c;
   BpLaunch aa = a;
   GroupSync *gs = reinterpret_cast<GroupSync *>(a.gsync);
   uint8_t *gcch = a.gcch;
   unsigned *abort = reinterpret_cast<unsigned *>(gs + groups);
   unsigned int *q = a.queue;
-  int f = fast;
+  int f = fast ? 1 : 0;
   void *args[] = {&cc, &aa, &gs, &gcch, &abort, &q, &f};
   return hipLaunchCooperativeKernel((const void *)kern, dim3((unsigned)(groups * kG)), dim3(T), args, (unsigned)lds,
                                     s);
@@ -1056,10 +1459,35 @@ hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s) {
     // exchange entries per thread: every member's lists must fit RX * T
     int xmax = 0;
     for (int m = 0; m < kPartG; m++) xmax = std::max(xmax, std::max(c.pt_xr_n[m], c.pt_xc_n[m]));
-#define KML_PART_CASE(T_, R_, X_)                                                                  \
-  if (k.T == T_ && xmax <= X_ * T_)                                                               \
-    return a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true>(c, a, s, fast, groups)             \
-                 : launch_part_t<kPartG, T_, R_, R_, X_, false>(c, a, s, fast, groups);
+    // Tagged exchange (default): one launch for the FAST codewords of same-XCD
+    // groups, then a barrier-exchange launch over the codewords it deferred
+    // (list and count in scratch past the groups' mailboxes / sync blocks).
+    bool tagged = part_tagged_fits(c.E, c.pt_ncut) && fast;
+    if (const char *t = getenv("KML_PART_TAGGED"))
+      if (t[0] == '0') tagged = false;
+    BpLaunch d = a;
+    if (tagged) {
+      if ((a.gslots_cap - (long long)groups * c.E) * 4 < a.B) return hipErrorNotSupported;
+      d.defer_idx = reinterpret_cast<int32_t *>(a.gslots + (size_t)groups * c.E);
+      d.defer_cnt = reinterpret_cast<unsigned *>(reinterpret_cast<char *>(a.gsync) + part_defer_offset(groups));
+      hipError_t e = hipMemsetAsync(d.defer_cnt, 0, sizeof(unsigned), s);
+      if (e != hipSuccess) return e;
+    }
+#define KML_PART_CASE(T_, R_, X_)                                                                   \
+  if (k.T == T_ && xmax <= X_ * T_) {                                                              \
+    if (tagged) {                                                                                  \
+      hipError_t e = a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true, true>(c, d, s, fast, groups, true)    \
+                           : launch_part_t<kPartG, T_, R_, R_, X_, false, true>(c, d, s, fast, groups, true);  \
+      if (e != hipSuccess) return e;                                                               \
+      BpLaunch b = a;                                                                              \
+      b.cw_idx = d.defer_idx;                                                                      \
+      b.B_dev = d.defer_cnt;                                                                       \
+      return a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true, false>(c, b, s, fast, groups, false)          \
+                   : launch_part_t<kPartG, T_, R_, R_, X_, false, false>(c, b, s, fast, groups, false);        \
+    }                                                                                              \
+    return a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true, false>(c, a, s, fast, groups, true)             \
+                 : launch_part_t<kPartG, T_, R_, R_, X_, false, false>(c, a, s, fast, groups, true);           \
+  }
     KML_PART_CASE(512, 4, 4)
     KML_PART_CASE(768, 3, 3)
     KML_PART_CASE(1024, 2, 2)

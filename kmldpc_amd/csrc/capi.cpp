@@ -170,6 +170,8 @@ int upload_code(kml_ctx *c) {
   reserve(part.xr_ptr.size() * 4);
   reserve(part.xc.size() * 4);
   reserve(part.xc_ptr.size() * 4);
+  reserve(part.vx.size() * 4);
+  reserve(part.rx.size() * 4);
   // round plan of the irregular-code kernel (layout.hpp IrregularPlan)
   kml::IrregularPlan irr;
   if (!regular && !kml::plan_irregular(L, kml::kIrrThreads, kml::kIrrVnPairMax, kml::kIrrCnPairMax, irr))
@@ -198,8 +200,10 @@ int upload_code(kml_ctx *c) {
   put(14, part.xr_ptr.data(), part.xr_ptr.size() * 4);
   put(15, part.xc.data(), part.xc.size() * 4);
   put(16, part.xc_ptr.data(), part.xc_ptr.size() * 4);
-  put(17, irr.vn.data(), irr.vn.size() * 4);
-  put(18, irr.cn.data(), irr.cn.size() * 4);
+  put(17, part.vx.data(), part.vx.size() * 4);
+  put(18, part.rx.data(), part.rx.size() * 4);
+  put(19, irr.vn.data(), irr.vn.size() * 4);
+  put(20, irr.cn.data(), irr.cn.size() * 4);
   HIPCHK(c, hipMemcpy(c->d_graph.p, host.data(), bytes, hipMemcpyHostToDevice), "upload graph");
   unsigned char *base = c->d_graph.as<unsigned char>();
   kml::DevCode &d = c->dc;
@@ -221,8 +225,10 @@ int upload_code(kml_ctx *c) {
   d.pt_xr_ptr = part.G ? reinterpret_cast<const int32_t *>(base + off[14]) : nullptr;
   d.pt_xc = part.G ? reinterpret_cast<const int32_t *>(base + off[15]) : nullptr;
   d.pt_xc_ptr = part.G ? reinterpret_cast<const int32_t *>(base + off[16]) : nullptr;
-  d.irr_vn = irr.vn.empty() ? nullptr : reinterpret_cast<const int32_t *>(base + off[17]);
-  d.irr_cn = irr.cn.empty() ? nullptr : reinterpret_cast<const int32_t *>(base + off[18]);
+  d.pt_vx = part.G ? reinterpret_cast<const int32_t *>(base + off[17]) : nullptr;
+  d.pt_rx = part.G ? reinterpret_cast<const int32_t *>(base + off[18]) : nullptr;
+  d.irr_vn = irr.vn.empty() ? nullptr : reinterpret_cast<const int32_t *>(base + off[19]);
+  d.irr_cn = irr.cn.empty() ? nullptr : reinterpret_cast<const int32_t *>(base + off[20]);
   d.pt_ncut = part.ncut;
   d.pt_mirror = part.mirror_max;
   for (int m = 0; m < 4; m++) {

@@ -34,6 +34,7 @@ struct DevCode {
   // Partition plan of the partitioned cooperative kernel (layout.hpp
   // PartitionPlan); null / 0 when the code does not take it.
   const int32_t *pt_vn, *pt_cn, *pt_pos, *pt_vaddr, *pt_xr, *pt_xr_ptr, *pt_xc, *pt_xc_ptr;
+  const int32_t *pt_vx, *pt_rx;  // tagged exchange: mailbox index per column edge, per-row (first x, cut mask)
   int pt_G, pt_ncut, pt_mirror;
   int pt_xr_n[4], pt_xc_n[4];  // exchange-list lengths per member (host copy, launch checks)
 };
@@ -69,6 +70,10 @@ struct BpLaunch {
   // Entry e of the launch decodes codeword cw_idx[e] (NULL: e); every
   // per-codeword array above is indexed by the codeword, B counts entries.
   const int32_t *cw_idx = nullptr;
+  const unsigned *B_dev = nullptr;  // when set, the entry count is *B_dev (<= B), read on the device
+  // partitioned kernel's tagged launch: codewords it leaves to the barrier-exchange launch
+  int32_t *defer_idx = nullptr;
+  unsigned *defer_cnt = nullptr;
   // Cooperative global-slot kernel (bp_coop.hip): per-group sync blocks
   // (bp_coop_sync_bytes) and per-group hard-decision bytes (groups x N).
   void *gsync = nullptr;

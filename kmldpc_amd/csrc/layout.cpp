@@ -297,7 +297,7 @@ bool plan_partition(const LdpcCode &L, int G, PartitionPlan &out) {
   for (int p = 0; p < M; p++) row_at[out.cn[p]] = p;
   const int EG = MG * dc;
 
-  // cut edges, sorted by (row owner, column owner, partitioned row slot)
+  // cut edges, sorted by (row owner, partitioned row slot)
   struct Cut {
     int R, S, slot, col_pos, k;
   };
@@ -310,7 +310,7 @@ bool plan_partition(const LdpcCode &L, int G, PartitionPlan &out) {
     }
   }
   std::sort(cuts.begin(), cuts.end(), [](const Cut &a, const Cut &b) {
-    return a.R != b.R ? a.R < b.R : a.S != b.S ? a.S < b.S : a.slot < b.slot;
+    return a.R != b.R ? a.R < b.R : a.slot < b.slot;
   });
   out.ncut = (int)cuts.size();
   if (out.ncut >= (1 << 15)) return false;  // packed (x << 16) entries
@@ -344,8 +344,15 @@ bool plan_partition(const LdpcCode &L, int G, PartitionPlan &out) {
       if (best_r[r] == g) out.vaddr[(size_t)p * dv + k] = ((row_at[r] - g * MG) * dc + (s - L.row_ptr[r])) * 16;
     }
   }
-  for (size_t x = 0; x < cuts.size(); x++)
+  out.vx.assign((size_t)N * dv, -1);
+  out.rx.assign(M, 0);
+  for (size_t x = 0; x < cuts.size(); x++) {
     out.vaddr[(size_t)cuts[x].col_pos * dv + cuts[x].k] = (EG + mirror_of[x]) * 16;
+    out.vx[(size_t)cuts[x].col_pos * dv + cuts[x].k] = (int32_t)x;
+    const int P = cuts[x].slot / dc, e = cuts[x].slot % dc;  // plan row index, edge position in the row
+    if (!(out.rx[P] & 0xFF)) out.rx[P] = (int32_t)(x << 8);
+    out.rx[P] |= 1 << e;
+  }
   return true;
 }
 

@@ -44,8 +44,10 @@ namespace kml {
 // CUT edge of its columns (an edge whose row another member owns).  Cut edges
 // are exchanged through two mailboxes in global memory, v2c (column owner ->
 // row owner) and c2v (row owner -> column owner), indexed by the cut-edge
-// index x, which is sorted by (row owner, column owner, row slot): each
-// sender's and each receiver's share is a few contiguous runs.  The planner
+// index x, which is sorted by (row owner, row slot): each row owner's share
+// is one contiguous run and the cut edges of one row are consecutive (the
+// tagged exchange addresses a row's mailbox entries from its first index and
+// a 6-bit mask); each column owner's share is a few runs.  The planner
 // minimises the number of cut edges (balanced G-way partition of the Tanner
 // graph: alternating majority assignment of columns given rows and rows given
 // columns, capacity-bounded).  Any partition gives the same decoder output: it
@@ -62,6 +64,10 @@ struct PartitionPlan {
   // exchange lists, per member [ptr[m], ptr[m+1]); entry = (x << 16) | (LDS slot index)
   std::vector<int32_t> xr, xr_ptr;  // as row owner: cut edges of its rows
   std::vector<int32_t> xc, xc_ptr;  // as column owner: cut edges of its columns (-> mirror slots)
+  // tagged exchange (bp_part_kernel's direct mailbox stores):
+  std::vector<int32_t> vx;  // 3N: [p*dv + k] = mailbox index x of that edge when it is cut, else -1
+  std::vector<int32_t> rx;  // M, plan order: (x of the row's first cut edge << 8) | mask of its cut
+                            // edges by position in the row (0 when none are cut)
 };
 
 // False when the code is not regular or M, N are not multiples of G.

@@ -114,6 +114,29 @@ static void check_partition(const LdpcCode &L) {
   const int nslots = P.MG * L.dc_max + P.mirror_max;
   for (size_t i = 0; i < P.vaddr.size(); i++)
     CHECK(P.vaddr[i] >= 0 && P.vaddr[i] < nslots * 16, "vaddr %zu = %d", i, P.vaddr[i]);
+  // tagged exchange: a row's cut edges have consecutive mailbox indices from
+  // rx's first index, in row order; vx names the same index from the column side
+  std::vector<int> seen_x(P.ncut, 0);
+  const int EG = P.MG * L.dc_max;
+  for (int m = 0; m < P.G; m++)
+    for (int q = P.xr_ptr[m]; q < P.xr_ptr[m + 1]; q++) {
+      const int x = P.xr[q] >> 16, slot = P.xr[q] & 0xFFFF;  // member-local row slot
+      const int Pr = m * P.MG + slot / L.dc_max, e = slot % L.dc_max;
+      const int mask = P.rx[Pr] & 0xFF;
+      CHECK((mask >> e) & 1, "row %d edge %d not in its cut mask", Pr, e);
+      const int want = (P.rx[Pr] >> 8) + __builtin_popcount(mask & ((1 << e) - 1));
+      CHECK(x == want, "row %d edge %d: x %d, rx gives %d", Pr, e, x, want);
+      seen_x[x]++;
+    }
+  long long nvx = 0;
+  for (size_t i = 0; i < P.vx.size(); i++)
+    if (P.vx[i] >= 0) {
+      ++nvx;
+      CHECK(P.vx[i] < P.ncut, "vx %zu = %d", i, P.vx[i]);
+      CHECK(P.vaddr[i] >= EG * 16, "cut edge %zu addressed to a row slot", i);
+    }
+  CHECK(nvx == P.ncut, "vx names %lld cut edges of %d", nvx, P.ncut);
+  for (int x = 0; x < P.ncut; x++) CHECK(seen_x[x] == 1, "mailbox index %d received %d times", x, seen_x[x]);
   printf("partition: %d of %d edges cut, mirror_max %d\n", P.ncut, L.E, P.mirror_max);
 }
 

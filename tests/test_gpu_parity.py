@@ -493,6 +493,33 @@ def test_global_slot_cooperative_kernel_still_exact(data_dir, monkeypatch):
         assert r["ret"][i] == ret and np.array_equal(r["cc_hat"][i], cch), i
 
 
+@pytest.mark.parametrize("tagged", ["1", "0"])
+def test_partitioned_kernel_tagged_exchange_and_deferral(data_dir, monkeypatch, tagged):
+    """bp_part_kernel's tagged exchange (FAST codewords: direct mailbox stores,
+    tag polling, per-iteration early-stop flags) and the barrier-exchange launch
+    it defers the other codewords to: a PEG8064 batch with two codewords outside
+    the fast-division domain (-0.0 / subnormal priors) among FAST ones, iteration
+    budgets 20 and 1, bit-exact against the oracle on ret, cc_hat and the soft
+    syndromes; KML_PART_TAGGED=0 (barrier exchange only) gives the same."""
+    monkeypatch.setenv("KML_PART_TAGGED", tagged)
+    ctx = ctx_for(data_dir, "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 20)
+    oc = oracle_for(data_dir, "PEG8064regular0.5.txt", False, 20)
+    rng = np.random.default_rng(33)
+    B = 300
+    p0 = np.clip(rng.normal(0.5, 0.28, (B, ctx.cc_len)), 0.02, 0.98)
+    p0[7, ::5] = -0.0
+    p0[23, 1::7] = 5e-320
+    for it in (20, 1):
+        r = ctx.bp_decode(p0, iter_count=it, cc_hat=True, syn=np.zeros((B, ctx.M)))
+        assert ctx.bp_kernel() == "bp_part_kernel"
+        for i in list(range(0, B, 13)) + [7, 23, B - 1]:
+            ret, uh, cch, syn = oc.bp_decode(p0[i], it)
+            assert r["ret"][i] == ret, (it, i)
+            assert np.array_equal(r["uu_hat"][i], uh), (it, i)
+            assert np.array_equal(r["cc_hat"][i], cch), (it, i)
+            assert np.array_equal(r["syn"][i], syn, equal_nan=True), (it, i)
+
+
 @pytest.mark.parametrize("matrix,modem,is5g,max_iter", CODES)
 def test_empty_and_ragged_batches(data_dir, matrix, modem, is5g, max_iter):
     ctx = ctx_for(data_dir, matrix, modem, is5g, max_iter)

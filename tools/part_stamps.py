@@ -19,6 +19,10 @@ sys.path.insert(0, REPO)
 os.environ.setdefault("KML_LIB", os.path.join(REPO, "kmldpc_amd", "libkmldpc_amd_stamps.so"))
 import kmldpc_amd as K  # noqa: E402
 
+# the tagged exchange (default) stamps: 0 loop top, 2 VN compute, 4 v2c poll,
+# 5 sync, 6 parity + CN compute, 7 sync, 8 flag post + c2v poll + flags poll + sync
+TAGGED_NAMES = ["iteration boundary", "-", "VN compute (wave 0)", "-", "poll v2c (wave 0)", "sync after v2c receive",
+                "CN compute + parity (wave 0)", "CN drain (sync)", "flag + c2v poll + flags + sync", "-"]
 NAMES = ["iteration boundary", "receive c2v (+sync)", "VN compute (wave 0)", "VN drain (sync)",
          "send v2c + group barrier", "receive v2c + decisions (+sync)", "parity + CN compute (wave 0)",
          "CN drain (sync)", "send c2v + group barrier (+flags)", "-"]
@@ -49,9 +53,16 @@ def main():
     per_iter = st.mean(axis=0) / iters_per_group
     tot = per_iter[:9].sum()
     print(f"codewords {B}, mean VN phases {c['vn_phases'] / B:.2f}, iterations per group {iters_per_group:.0f}")
+    names = NAMES if os.environ.get("KML_PART_TAGGED", "1") == "0" else TAGGED_NAMES
     for i in range(9):
-        print(f"  {NAMES[i]:36s} {per_iter[i]:9.0f} cycles  {100 * per_iter[i] / tot:5.1f}%")
+        print(f"  {names[i]:36s} {per_iter[i]:9.0f} cycles  {100 * per_iter[i] / tot:5.1f}%")
     print(f"  {'total per iteration':36s} {tot:9.0f} cycles")
+    # per member (workgroup w is member (w >> 3) % 4): a member that computes
+    # longer makes the others wait at the exchange
+    member = (np.arange(256) >> 3) % 4
+    for m in range(4):
+        row = st[member == m].mean(axis=0) / iters_per_group
+        print(f"  member {m}: " + " ".join(f"{row[i]:6.0f}" for i in range(9)))
     spread = st[:, 4] / iters_per_group
     print(f"  barrier-1 per-WG spread: min {spread.min():.0f} max {spread.max():.0f}")
 
