@@ -502,6 +502,7 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(d, args)
     print(json.dumps(line), flush=True)
+    ctx.close()  # release the device buffers while the runtime is fully up
     if dist is not None:
         dist.destroy_process_group()
 

@@ -1177,6 +1177,7 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
   __shared__ int spcnt;                  // unsatisfied checks of the member's rows (tagged path)
   unsigned nb = 0;                       // barrier sequence number (uniform, same on every member)
   unsigned g = 0;                        // global iteration counter of the tagged exchange (same on every member)
+  if (a.B_dev && *a.B_dev == 0) return;  // nothing deferred: every workgroup leaves before the first barrier
   if (tid == 0) {
     bst[0] = bst[1] = bst[2] = bst[3] = 0;
     sfail = 0;
@@ -1190,7 +1191,7 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
   // tagged exchange and defers every other codeword to a barrier-exchange
   // launch that follows it (a.defer_*); that launch takes its entry count
   // from the device (a.B_dev).
-  const int B = a.B_dev ? (int)*a.B_dev : a.B;
+  const int B = a.B_dev ? (int)*a.B_dev : a.B;  // (read again: every read sees the finished count)
 
   for (;;) {
     if (member == 0 && tid == 0) {
@@ -1332,6 +1333,27 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
   }
 }
 
+// Launch of a grid whose workgroups must all be co-resident (the group
+// barriers and tag polls wait on each other).  The occupancy of the kernel at
+// this block size and LDS is checked on the host (what hipLaunchCooperativeKernel
+// checks); the launch itself is a plain one, which gets the same residency
+// (MI355X_MICROARCH.md, coop-launch) without the cooperative-launch host cost,
+// and which rocprofv3's counter collection handles (a cooperative launch under
+// --pmc crashed the profiled process at exit).  KML_COOP_LAUNCH=1 restores the
+// cooperative launch.  A group that is not co-resident anyway times out its
+// polls and aborts the launch (bp_coop_aborted), which the caller reports.
+hipError_t launch_resident(const void *kern, unsigned grid, unsigned block, void **args, unsigned lds, hipStream_t s) {
+  if (const char *e = getenv("KML_COOP_LAUNCH"))
+    if (e[0] == '1') return hipLaunchCooperativeKernel(kern, dim3(grid), dim3(block), args, lds, s);
+  int per_cu = 0, dev = 0, ncu = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)block, lds);
+  if (e != hipSuccess) return e;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if ((long long)per_cu * ncu < (long long)grid) return hipErrorCooperativeLaunchTooLarge;
+  return hipLaunchKernel(kern, dim3(grid), dim3(block), args, lds, s);
+}
+
 template <int kG, int T, int RV, int RC, int RX, bool SYN, bool TAGGED>
 hipError_t launch_part_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast, int groups, bool reset_abort) {
   auto kern = bp_part_kernel<kG, T, RV, RC, RX, SYN, TAGGED>;
@@ -1355,8 +1377,7 @@ hipError_t launch_part_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int
   unsigned int *q = a.queue;
   int f = fast ? 1 : 0;
   void *args[] = {&cc, &aa, &gs, &gcch, &abort, &q, &f};
-  return hipLaunchCooperativeKernel((const void *)kern, dim3((unsigned)(groups * kG)), dim3(T), args, (unsigned)lds,
-                                    s);
+  return launch_resident((const void *)kern, (unsigned)(groups * kG), (unsigned)T, args, (unsigned)lds, s);
 }
 
 template <int kG, int T, int RV, int RC, bool SYN>
@@ -1375,7 +1396,7 @@ hipError_t launch_coop_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int
   unsigned int *q = a.queue;
   int f = fast;
   void *args[] = {&cc, &aa, &gs, &gcch, &abort, &q, &f};
-  return hipLaunchCooperativeKernel((const void *)kern, dim3((unsigned)(groups * kG)), dim3(T), args, 0, s);
+  return launch_resident((const void *)kern, (unsigned)(groups * kG), (unsigned)T, args, 0u, s);
 }
 
 // Kernel choice and tiling.  Default: the partitioned kernel (groups of 4,
