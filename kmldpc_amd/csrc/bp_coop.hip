@@ -1334,24 +1334,24 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
 }
 
 // Launch of a grid whose workgroups must all be co-resident (the group
-// barriers and tag polls wait on each other).  The occupancy of the kernel at
-// this block size and LDS is checked on the host (what hipLaunchCooperativeKernel
-// checks); the launch itself is a plain one, which gets the same residency
-// (MI355X_MICROARCH.md, coop-launch) without the cooperative-launch host cost,
-// and which rocprofv3's counter collection handles (a cooperative launch under
-// --pmc crashed the profiled process at exit).  KML_COOP_LAUNCH=1 restores the
-// cooperative launch.  A group that is not co-resident anyway times out its
-// polls and aborts the launch (bp_coop_aborted), which the caller reports.
+// barriers and tag polls wait on each other): a cooperative launch, which
+// also keeps another process's kernels from taking CUs the grid needs (two
+// ranks sharing one GPU).  KML_COOP_LAUNCH=0 launches plainly after the same
+// occupancy check, for rocprofv3 --pmc runs only: a cooperative launch under
+// counter collection crashed the profiled process at exit.  A group that is
+// not co-resident times out its polls and aborts the launch (bp_coop_aborted).
 hipError_t launch_resident(const void *kern, unsigned grid, unsigned block, void **args, unsigned lds, hipStream_t s) {
   if (const char *e = getenv("KML_COOP_LAUNCH"))
-    if (e[0] == '1') return hipLaunchCooperativeKernel(kern, dim3(grid), dim3(block), args, lds, s);
-  int per_cu = 0, dev = 0, ncu = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)block, lds);
-  if (e != hipSuccess) return e;
-  hipGetDevice(&dev);
-  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  if ((long long)per_cu * ncu < (long long)grid) return hipErrorCooperativeLaunchTooLarge;
-  return hipLaunchKernel(kern, dim3(grid), dim3(block), args, lds, s);
+    if (e[0] == '0') {
+      int per_cu = 0, dev = 0, ncu = 0;
+      hipError_t r = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)block, lds);
+      if (r != hipSuccess) return r;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      if ((long long)per_cu * ncu < (long long)grid) return hipErrorCooperativeLaunchTooLarge;
+      return hipLaunchKernel(kern, dim3(grid), dim3(block), args, lds, s);
+    }
+  return hipLaunchCooperativeKernel(kern, dim3(grid), dim3(block), args, lds, s);
 }
 
 template <int kG, int T, int RV, int RC, int RX, bool SYN, bool TAGGED>
