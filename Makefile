@@ -43,11 +43,14 @@ clean:
 
 .PHONY: all lib oracle clean
 
-# Phase-timing build of the partitioned cooperative kernel (s_memtime stamps,
-# kml_debug_part_stamps); load it with KML_LIB=kmldpc_amd/libkmldpc_amd_stamps.so
+# Phase-timing build of the partitioned cooperative kernel and the fused
+# k-means (s_memtime stamps, kml_debug_part_stamps / kml_debug_km_stamps);
+# load it with KML_LIB=kmldpc_amd/libkmldpc_amd_stamps.so
+STAMPED  := bp_coop kmeans
 STAMPS_LIB := kmldpc_amd/libkmldpc_amd_stamps.so
-STAMPS_OBJS := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(CPP_SRCS) $(filter-out bp_coop,$(HIP_SRCS)))) $(OBJDIR)/stamps/bp_coop.o
-$(OBJDIR)/stamps/bp_coop.o: $(CSRC)/bp_coop.hip $(HDRS)
+STAMPS_OBJS := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(CPP_SRCS) $(filter-out $(STAMPED),$(HIP_SRCS)))) \
+               $(addprefix $(OBJDIR)/stamps/,$(addsuffix .o,$(STAMPED)))
+$(OBJDIR)/stamps/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)/stamps
 	$(HIPCC) $(HIPFLAGS) -DKML_STAMPS=1 -c -o $@ $<
 $(STAMPS_LIB): $(STAMPS_OBJS)

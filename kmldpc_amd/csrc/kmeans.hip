@@ -15,7 +15,10 @@
 // has to decide, per symbol, whether cluster 0 is the FIRST minimum of the K
 // distances (kmeans.cc:41-44).
 //
-// MI355X mapping — one k-means iteration is two launches:
+// MI355X mapping.  The production path is km_fused_kernel (one workgroup per
+// codeword, the whole Run in one launch; described at its definition).  The
+// two-launch form below (KML_KMEANS=split, A/B and S > 4096) runs one k-means
+// iteration as two launches:
 //   km_assign  one thread per (codeword, symbol): the K distances are screened
 //              with squared norms d2 = dr*dr + di*di (relative error <= 3 ulp of
 //              the exact |.|^2 of the same rounded dr, di; glibc hypot is
@@ -245,16 +248,76 @@ __global__ void km_final_kernel(const double *__restrict__ cons, const double *_
 }
 
 // ---------------------------------------------------------------------------
-// Fused k-means: one workgroup per codeword runs the whole KMeans::Run.  The
-// symbols are staged in LDS once; each iteration assigns in parallel (same
-// screening as km_assign, 64-symbol words by ballot), compacts the cluster-0
-// members' values into LDS in ascending symbol order, and two lanes run the
-// re / im accumulation chains in that order (the reference's sequential sum,
-// software-pipelined so the adds, not the LDS latency, set its pace); lane 0
-// then tests convergence and updates h_hat.  One launch instead of two per
-// iteration, and y is read from HBM once.
-constexpr int kFusedT = 256;
+// Fused k-means: one workgroup of two waves per codeword runs the whole
+// KMeans::Run.  The symbols are staged in LDS once; each iteration assigns in
+// parallel (same screening as km_assign, 64-symbol words by ballot), lists the
+// cluster-0 members' indices in ascending symbol order (u16, LDS), and sums
+// their values onto the cumulative sum in that order (the reference's
+// sequential rounding: wave 0 the real chain, wave 1 the imaginary chain, by
+// exact binade-segmented scans, ordered_sum_wave); lane 0 then updates h_hat.
+// y is read from HBM once; LDS per codeword is 16 S + 2 S bytes (+ 1 KB), so
+// 7 codewords share a CU for QPSK/PEG2304.
+//
+// Per-iteration latency is what bounds this kernel (each codeword is a chain
+// of dependent steps; a dependent VALU step costs ~40 cycles with 3-4 waves
+// per SIMD), so the iterations skip the work whose outcome is already known,
+// exactly:
+//   * convergence (kmeans.cc:47-56) compares clusters_ = c_k * hatH with the
+//     previous iteration's; lanes k < KC compute both at the iteration START
+//     (the cluster points the assignment needs anyway), so a converged
+//     iteration breaks before its assignment (whose sums the reference
+//     discards: only hatH is read after the loop);
+//   * incremental assignment: when a symbol is assigned, the gap between its
+//     distance to cluster 0 and to the nearest other cluster gives a margin g
+//     (a lower bound of the true gap, with the fp64 rounding of the screened
+//     squared distances and of glibc hypot folded in).  A later hatH moves
+//     cluster k by at most |c_k| |hatH' - hatH| plus the rounding of the two
+//     complex products, so while 2 Cmax (D(t) - D(ref)) < g — D the running
+//     sum of the per-iteration bounds |dh| + 2^-48 (|h| + |h'|), rounded up —
+//     the symbol's decision cannot change.  A 64-symbol word is re-assigned
+//     when any of its symbols may have changed: each word keeps the minimum
+//     over its symbols of T = D(ref) + g / (2 Cmax) (float, rounded down);
+//   * the member list is rebuilt only when some word's membership bits
+//     changed (each wave scans the word popcounts itself and scatters its own
+//     words: no barrier in between);
+//   * the cumulative-mean division by (cnt, 0) and the division by c[0] take
+//     __divdc3's own branch with the constant parts hoisted (exact: same
+//     operations on the same values).
+// Measured (MI355X, 32768 PEG2304/QPSK codewords at Es/N0 2 dB, 19.9
+// iterations each): 4.28 ms -> 3.44 ms; tools/km_stamps.py gives the phases.
+constexpr int kFusedT = 128;  // two waves per codeword (the two sum chains), up to 7 codewords per CU (LDS)
 constexpr int kFusedMaxW = 64;  // 64-symbol words: S <= 4096
+
+// Phase timing (stamps build, -DKML_STAMPS=1; tools/km_stamps.py): thread 0's
+// s_memtime deltas summed over workgroups, plus event counts.
+#ifndef KML_STAMPS
+#define KML_STAMPS 0
+#endif
+enum { KS_PRO, KS_CLUSTERS, KS_ASSIGN, KS_COMPACT, KS_SUM, KS_ITERS, KS_WORDS, KS_COMPACTIONS, KS_CW, KS_UPDATE, KS_STEPS,
+       KS_SLOTS = 16 };
+__device__ unsigned long long kml_km_stamps[KS_SLOTS];
+#if KML_STAMPS
+// accumulated in thread 0's registers, flushed once per workgroup (KM_FLUSH)
+#define KM_STAMP(i)                                                \
+  do {                                                             \
+    if (tid == 0) {                                                \
+      const unsigned long long _t = __builtin_amdgcn_s_memtime();  \
+      km_acc[(i)] += _t - km_prev;                                 \
+      km_prev = _t;                                                \
+    }                                                              \
+  } while (0)
+#define KM_COUNT(i, v) \
+  do {                 \
+    if (tid == 0) km_acc[(i)] += (unsigned long long)(v); \
+  } while (0)
+#else
+#define KM_STAMP(i) \
+  do {              \
+  } while (0)
+#define KM_COUNT(i, v) \
+  do {                 \
+  } while (0)
+#endif
 
 __device__ __forceinline__ double wave_max(double v) {
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
@@ -264,41 +327,335 @@ __device__ __forceinline__ int wave_min_i(int v) {
   for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
   return v;
 }
+// wave minimum by DPP (quad swaps, row mirrors, row broadcasts 15 / 31: no
+// LDS round trips), the result read from lane 63
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_min_step(float v) {
+  const float o = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROWS, 0xF, false));
+  return fminf(v, o);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_add_step_i(int v) {
+  return v + __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ int wave_inclusive_scan_i(int v) {
+  v = dpp_add_step_i<0x111, 0xF>(v);  // row_shr:1
+  v = dpp_add_step_i<0x112, 0xF>(v);  // row_shr:2
+  v = dpp_add_step_i<0x114, 0xF>(v);  // row_shr:4
+  v = dpp_add_step_i<0x118, 0xF>(v);  // row_shr:8
+  v = dpp_add_step_i<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+  v = dpp_add_step_i<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+  return v;
+}
+__device__ __forceinline__ float wave_min_f(float v) {
+  v = dpp_min_step<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v = dpp_min_step<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v = dpp_min_step<0x141, 0xF>(v);  // row_half_mirror
+  v = dpp_min_step<0x140, 0xF>(v);  // row_mirror: every lane holds its row's minimum
+  v = dpp_min_step<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+  v = dpp_min_step<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 
-// acc + x[0] + x[2] + ... + x[2(n-1)] in that order (stride 2: one component
-// of a double2 array).
-__device__ __forceinline__ double ordered_sum(double acc, const double *x, int n) {
-  int i = 0;
-  for (; i + 4 <= n; i += 4) {
-    const double a0 = x[2 * i], a1 = x[2 * i + 2], a2 = x[2 * i + 4], a3 = x[2 * i + 6];
-    acc = acc + a0;
-    acc = acc + a1;
-    acc = acc + a2;
-    acc = acc + a3;
+// acc + y[2 m_0] + y[2 m_1] + ... + y[2 m_(n-1)] in that order (the
+// reference's rounding), m the compacted member indices (u16, 16-byte
+// aligned, at least n + 24 readable; indices past n are clamped into [0, S)).
+// Software pipeline over blocks of 8: the indices of block b + 2 and the
+// values of block b + 1 (from indices already in registers) are in flight
+// while block b is added, so neither LDS latency sits on the chain of
+// dependent adds.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void fetch8(const double *yv, u32x4 q, int S, double (&v)[8]) {
+  const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = yv[2 * min((int)(w[k] & 0xffffu), S - 1)];
+    v[2 * k + 1] = yv[2 * min((int)(w[k] >> 16), S - 1)];
   }
-  for (; i < n; ++i) acc = acc + x[2 * i];
+}
+__device__ __forceinline__ double ordered_sum(double acc, const double *yv, const unsigned short *m, int n, int S) {
+  // The index list is the same for both lanes; left uniform, hipcc moves the
+  // indices to SGPRs (v_readfirstlane) right after their loads, which waits
+  // for them on the spot.  A VGPR base address keeps them in VGPRs, waited
+  // for only where the values' addresses are formed, a block later.
+  unsigned mb = lds_addr(m);
+  asm volatile("" : "+v"(mb));
+  double cur[8];
+  fetch8(yv, lds_ld<u32x4>(mb), S, cur);
+  u32x4 qn = lds_ld<u32x4>(mb + 16);
+  int i = 0;
+#pragma clang loop unroll(disable)  // unrolled, the second copy waits for the first copy's index load
+  for (; i + 8 <= n; i += 8) {
+    const u32x4 q2 = lds_ld<u32x4>(mb + 2 * i + 32);
+    double nxt[8];
+    fetch8(yv, qn, S, nxt);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc = acc + cur[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
+    qn = q2;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k)  // the tail (< 8 values), already loaded
+    if (i + k < n) acc = acc + cur[k];
   return acc;
+}
+
+// The same sum computed by a whole wave (binade-segmented integer scans;
+// tools/probe/km_scan_model.py is a CPU model of exactly these steps, checked
+// against the sequential sum on adversarial inputs).  While the running sum
+// stays in one binade [2^(e-1), 2^e) (magnitude; sign sg), every rounded add
+// is a move on the fixed grid u = 2^(e-53): with A = |acc| / u (an integer in
+// [2^52, 2^53)) and X = sg x / u (exact ldexp), RN(acc + x) = sg (A + rint(X)) u
+// unless X is a tie (frac 0.5: the parity of the result decides) or the result
+// leaves the binade.  Each lane takes kScanPer consecutive elements, rounds
+// them to the grid (v_rndne), sums them locally, and a DPP exclusive scan of
+// the lane totals gives every prefix A + P.  All elements before the first one
+// that is a tie, large (|X| >= 2^51: keeps every partial sum of valid elements
+// below 2^53, hence exact), or whose prefix leaves [2^52 + 1, 2^53 - 1] (then
+// the exact sum lies inside the binade, where RN is the grid rounding) are
+// exact; that element is added with a real fp64 add and the scan resumes after
+// it.  A zero or non-finite sum, and runs after an early exit, are added one
+// by one.  On MI355X a dependent f64 add chain costs ~40 cycles per element
+// here (LDS index + value loads, other waves on the SIMD); a step of 256
+// elements costs about 50 dependent instructions.
+constexpr int kScanPer = 4;  // 8 per lane measured slower (3.89 vs 3.44 ms per 32768 QPSK cw)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_add_step(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWS, 0xF, false);
+  return v + __hiloint2double(hi, lo);
+}
+// sum over the lanes below this one (exact where those sums are)
+__device__ __forceinline__ double wave_exclusive_scan(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xF, 0xF, false);  // wave_shr:1
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xF, 0xF, false);
+  v = __hiloint2double(hi, lo);
+  v = dpp_add_step<0x111, 0xF>(v);  // row_shr:1
+  v = dpp_add_step<0x112, 0xF>(v);  // row_shr:2
+  v = dpp_add_step<0x114, 0xF>(v);  // row_shr:4
+  v = dpp_add_step<0x118, 0xF>(v);  // row_shr:8: prefix within each row of 16
+  v = dpp_add_step<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+  v = dpp_add_step<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+  return v;
+}
+__device__ __forceinline__ double lane_d(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ double ordered_sum_wave(double acc, const double *yv, const unsigned short *m, int n, int S, int lane,
+                                   int &steps) {
+  int i = 0, seq = 0;
+  while (i < n) {  // wave-uniform
+    ++steps;
+    const int c = min(64 * kScanPer, n - i);
+    double x[kScanPer];
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      const int j = i + kScanPer * lane + k;
+      x[k] = j < n ? yv[2 * min((int)m[j], S - 1)] : 0.0;
+    }
+    if (seq > 0 || !(acc != 0.0 && isfinite(acc))) {  // one by one, lane-major element order
+      const int mm = seq > 0 ? min(seq, c) : 1;
+      for (int l = 0; l * kScanPer < mm; ++l) {
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k)
+          if (l * kScanPer + k < mm) acc = acc + lane_d(x[k], l);
+      }
+      seq = seq > 0 ? seq - mm : 0;
+      i += mm;
+      continue;
+    }
+    const int e = __builtin_amdgcn_frexp_exp(acc);  // |acc| in [2^(e-1), 2^e)
+    const double sg = acc < 0.0 ? -1.0 : 1.0;
+    const double A = __builtin_amdgcn_ldexp(fabs(acc), 53 - e);
+    double L[kScanPer];
+    unsigned badm = 0;
+    double run = 0.0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      const double X = __builtin_amdgcn_ldexp(sg * x[k], 53 - e);
+      const bool bad = !(fabs(X) < 0x1p51) || (X - floor(X)) == 0.5;
+      badm |= (bad ? 1u : 0u) << k;
+      run = run + (bad ? 0.0 : rint(X));
+      L[k] = run;
+    }
+    const double E = wave_exclusive_scan(run);
+    const int kl = min(max(c - kScanPer * lane, 0), kScanPer);  // this lane's elements
+    unsigned outm = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      const double T = A + (E + L[k]);
+      const bool out = k < kl && (((badm >> k) & 1u) || !(T >= 0x1p52 + 1.0 && T <= 0x1p53 - 1.0));
+      outm |= (out ? 1u : 0u) << k;
+    }
+    const uint64_t ob = __ballot(outm != 0);
+    if (ob == 0) {
+      const int kk = (c - 1) % kScanPer;
+      double Tl = A + (E + L[0]);
+#pragma unroll
+      for (int k = 1; k < kScanPer; ++k)
+        if (kk == k) Tl = A + (E + L[k]);
+      acc = sg * __builtin_amdgcn_ldexp(lane_d(Tl, (c - 1) / kScanPer), e - 53);
+      i += c;
+    } else {
+      const int lf = __builtin_ctzll(ob);
+      const int fk = __builtin_ctz(outm | (1u << kScanPer));  // meaningful in lane lf
+      double Tpre = A + E, xf = x[0];
+#pragma unroll
+      for (int k = 1; k < kScanPer; ++k)
+        if (fk == k) {
+          Tpre = A + (E + L[k - 1]);
+          xf = x[k];
+        }
+      acc = sg * __builtin_amdgcn_ldexp(lane_d(Tpre, lf), e - 53);
+      acc = acc + lane_d(xf, lf);  // the exiting / tie / large element, rounded for real
+      const int f = kScanPer * lf + __builtin_amdgcn_readlane(fk, lf);
+      i += f + 1;
+      if (f < 16) seq = 32;  // exits close together: a short one-by-one run
+    }
+  }
+  return acc;
+}
+
+// Lower bound of |sqrt(hi) - sqrt(lo)| (true distances of the fp cluster
+// points) from the screened squared distances lo <= hi:
+//   sqrt(hi) - sqrt(lo) = (hi - lo) / (sqrt(hi) + sqrt(lo)) >= (hi - lo) / (2 sqrt(hi)).
+// The fp64 d2 values are within 2^-50 relative of the exact squares, hence
+// the 1e-13 (hi + lo) term; the float conversion and v_rsq_f32 are within
+// 2^-22 relative, hence 0.5 (1 - 1e-5); the final 1e-13 (hi + 1) >= 2e-13
+// sqrt(hi) term absorbs glibc hypot's rounding at the later comparison.
+// 0 outside the float range (the symbol is then re-assigned every iteration).
+__device__ __forceinline__ double dist_margin(double lo, double hi) {
+  if (!(lo >= 1e-30 && hi <= 1e30)) return 0.0;
+  const double num = (hi - lo) - 1e-13 * (hi + lo);
+  const double q = num * (double)__builtin_amdgcn_rsqf((float)hi) * (0.5 * (1.0 - 1e-5)) - 1e-13 * (hi + 1.0);
+  return q > 0.0 ? q : 0.0;
+}
+
+// the tie-band / exact decision out of line (rare; keeps the hot loop's
+// registers free)
+#ifndef KML_KM_OUTLINE
+#define KML_KM_OUTLINE 1
+#endif
+#if KML_KM_OUTLINE
+#define KM_SLOW __noinline__
+#else
+#define KM_SLOW __forceinline__
+#endif
+template <int KC>
+__device__ KM_SLOW bool member0_slow(const double2 *cl, double yr, double yi) {
+  return member0<KC>(cl, yr, yi);
+}
+
+// member0 (above) plus the decision's margin g (0 when the tie band or the
+// exact path decided).
+template <int KC>
+__device__ __forceinline__ bool member0_margin(const double2 *cl, double yr, double yi, double &g) {
+  double d0 = 0.0, m1 = 0.0;
+  bool fin = true;
+#pragma unroll 8
+  for (int k = 0; k < KC; ++k) {
+    const double2 c = cl[k];
+    const double dr = c.x - yr, di = c.y - yi;
+    const double d = dr * dr + di * di;
+    if (k == 0)
+      d0 = d;
+    else if (k == 1 || d < m1)
+      m1 = d;
+    fin = fin && d2_ok(d);
+  }
+  g = 0.0;
+  if (fin) {
+    if (d0 < m1 * (1.0 - kTieBand)) {
+      g = dist_margin(d0, m1);
+      return true;
+    }
+    if (d0 > m1 * (1.0 + kTieBand)) {
+      g = dist_margin(m1, d0);
+      return false;
+    }
+  }
+  return member0_slow<KC>(cl, yr, yi);
+}
+
+__device__ KM_SLOW cplx cdiv_slow(cplx n, cplx dd) { return kml_cdiv(n, dd); }
+
+// kml_cdiv(n, {c, 0}) for a count c >= 1: __divdc3's |c| >= |d| branch with
+// ratio = 0 / c = 0 and denom = 0 * 0 + c = c, where fabs(ratio) > DBL_MIN is
+// false, gives x = (a + 0 * (b / c)) / c and y = (b - 0 * (a / c)) / c, which
+// are a / c and b / c for finite nonzero a, b (the zero terms only matter for
+// signed zeros).  Anything else takes the full restatement.
+__device__ __forceinline__ cplx cdiv_count(double a, double b, int cnt) {
+  const double c = (double)cnt;
+  if (cnt > 0 && a != 0.0 && b != 0.0 && isfinite(a) && isfinite(b)) return cplx{a / c, b / c};
+  return cdiv_slow(cplx{a, b}, cplx{c, 0.0});
+}
+
+// kml_cdiv(n, c0) with c0 fixed for the launch: the branch, ratio and denom
+// depend on c0 only and are hoisted (the same operations on the same values).
+struct CdivConst {
+  double ratio, denom;
+  int mode;  // 1: |c| < |d|, 2: |c| >= |d|, 0: the DBL_MIN branch (full restatement)
+};
+__device__ __forceinline__ CdivConst cdiv_prepare(cplx dd) {
+  const double RMIN = 2.2250738585072014e-308;
+  const double c = dd.re, d = dd.im;
+  CdivConst k;
+  if (fabs(c) < fabs(d)) {
+    k.ratio = c / d;
+    k.denom = (c * k.ratio) + d;
+    k.mode = 1;
+  } else {
+    k.ratio = d / c;
+    k.denom = (d * k.ratio) + c;
+    k.mode = 2;
+  }
+  if (!(fabs(k.ratio) > RMIN)) k.mode = 0;
+  return k;
+}
+__device__ __forceinline__ cplx cdiv_const(cplx n, cplx dd, const CdivConst &k) {
+  double x, y;
+  if (k.mode == 1) {
+    x = ((n.re * k.ratio) + n.im) / k.denom;
+    y = ((n.im * k.ratio) - n.re) / k.denom;
+  } else if (k.mode == 2) {
+    x = ((n.im * k.ratio) + n.re) / k.denom;
+    y = (n.im - (n.re * k.ratio)) / k.denom;
+  } else {
+    return cdiv_slow(n, dd);
+  }
+  if (isnan(x) && isnan(y)) return cdiv_slow(n, dd);  // the Annex G recovery cases
+  return cplx{x, y};
 }
 
 template <int KC>
 __global__ __launch_bounds__(kFusedT) void km_fused_kernel(const double *__restrict__ cons,
                                                            const double *__restrict__ rot,
                                                            const double2 *__restrict__ y, int S, int iters,
-                                                           double2 *__restrict__ h_hat, double2 *__restrict__ h4) {
+                                                           double2 *__restrict__ h_hat, double2 *__restrict__ h4,
+                                                           int incremental, int scan) {
   extern __shared__ __attribute__((aligned(16))) unsigned char kmem[];
   double2 *ys = reinterpret_cast<double2 *>(kmem);  // [S] symbols
-  double2 *ym = ys + S;                              // [S] compacted cluster-0 members
+  // compacted cluster-0 member indices, ascending: [S + 24], 16-byte aligned
+  unsigned short *mem = reinterpret_cast<unsigned short *>(ys + S);
   __shared__ double2 cl[KC];
   __shared__ uint64_t wbits[kFusedMaxW];
-  __shared__ int wpos[kFusedMaxW + 1];
+  __shared__ float wthr[kFusedMaxW];  // per word: min over its symbols of D(ref) + g / (2 Cmax)
   __shared__ double red_d[kFusedT / 64];
   __shared__ int red_i[kFusedT / 64];
   __shared__ double2 s_hat;
-  __shared__ int s_done, s_exact;
+  __shared__ int s_exact;
+  __shared__ int s_flag[1 + kFusedT / 64];  // converged; per wave: member bits changed
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = kFusedT / 64;
   const int cw = blockIdx.x;
   const int Sw = (S + 63) / 64;
+#if KML_STAMPS
+  unsigned long long km_prev = __builtin_amdgcn_s_memtime();
+  unsigned long long km_acc[KS_STEPS + 1] = {};
+  KM_COUNT(KS_CW, 1);
+#endif
   const double2 *yy = y + (long long)cw * S;
   for (int j = tid; j < S; j += kFusedT) ys[j] = yy[j];
   if (tid == 0) s_exact = 0;
@@ -362,74 +719,147 @@ __global__ __launch_bounds__(kFusedT) void km_fused_kernel(const double *__restr
     mi = red_i[0];
   }
   const cplx c0{cons[0], cons[1]};
+  const CdivConst c0k = cdiv_prepare(c0);
   cplx hat = kml_cdiv(cplx{ys[mi].x, ys[mi].y}, c0);  // kmeans.cc:25
-  cplx prev{0.0, 0.0};
-  bool have_prev = false;
+  // 1 / (2 Cmax), rounded down (|c| <= |re| + |im|)
+  double cb = 0.0;
+  for (int k = 0; k < KC; ++k) cb = fmax(cb, fabs(cons[2 * k]) + fabs(cons[2 * k + 1]));
+  const double inv2c = cb > 0.0 ? (0.5 / cb) * (1.0 - 1e-12) : 0.0;
+  // lane k < KC: cluster k of the previous iteration (tempClusters, zero at first)
+  cplx prevk{0.0, 0.0};
+  cplx hprev = hat;
+  double drift = 0.0;  // D: the same value in every thread
+  if (tid < kFusedMaxW) wthr[tid] = -1.0f;  // every word is assigned in the first iteration
   double sr = 0.0, si = 0.0;  // cumulative cluster-0 sum (kmeans.cc:33-34, 46)
   int cnt = 0;
+  int nmem = 0;  // members in the current list
+  KM_STAMP(KS_PRO);
   for (int it = 0; it < iters; ++it) {
-    for (int k = tid; k < KC; k += kFusedT) {
-      const cplx p = kml_cmul(cplx{cons[2 * k], cons[2 * k + 1]}, hat);  // clusters_[k] = c[k] * hatH
-      cl[k] = make_double2(p.re, p.im);
-    }
-    __syncthreads();
-    // assignment: is cluster 0 the first minimum?  (kmeans.cc:36-46)
-    for (int w = wave; w < Sw; w += NW) {
-      const int j = w * 64 + lane;
-      const bool m = j < S && member0<KC>(cl, ys[j].x, ys[j].y);
-      const uint64_t bits = __ballot(m);
-      if (lane == 0) wbits[w] = bits;
-    }
-    __syncthreads();
-    if (tid < 64) {  // word offsets: exclusive prefix of the popcounts (Sw <= 64)
-      int c = tid < Sw ? __popcll(wbits[tid]) : 0;
-      int x = c;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(x, o);
-        if (lane >= o) x += t;
+    // clusters_[k] = c[k] * hatH, and the convergence test against
+    // tempClusters (kmeans.cc:26-28 / 72-74, 47-56)
+    if (wave == 0) {  // KC <= 64: one wave computes the clusters and the test
+      bool same = true;
+      if (lane < KC) {
+        const cplx p = kml_cmul(cplx{cons[2 * lane], cons[2 * lane + 1]}, hat);
+        cl[lane] = make_double2(p.re, p.im);
+        same = (p.re == prevk.re) && (p.im == prevk.im);
+        prevk = p;
       }
-      wpos[tid] = x - c;
-      if (tid == 63) wpos[kFusedMaxW] = x;
+      const bool all = __ballot(!same) == 0;
+      if (lane == 0) s_flag[0] = all;
     }
     __syncthreads();
-    for (int w = wave; w < Sw; w += NW) {
-      const uint64_t bits = wbits[w];
-      if ((bits >> lane) & 1) ym[wpos[w] + __popcll(bits & ((1ull << lane) - 1))] = ys[w * 64 + lane];
+    const int conv = s_flag[0];
+    KM_STAMP(KS_CLUSTERS);
+    if (conv) break;  // the reference breaks after an assignment it then discards
+    KM_COUNT(KS_ITERS, 1);
+    // drift bound D (rounded up), identical in every thread
+    {
+      const double dd = (fabs(hat.re - hprev.re) + fabs(hat.im - hprev.im)) * (1.0 + 1e-15) +
+                        0x1p-48 * (fabs(hat.re) + fabs(hat.im) + fabs(hprev.re) + fabs(hprev.im));
+      drift = (drift + dd) * (1.0 + 0x1p-50);
+      hprev = hat;
     }
+    // assignment: is cluster 0 the first minimum?  (kmeans.cc:36-46), only
+    // the words whose decisions the drift may have changed
+    int chg = 0;
+    {
+      // this wave's words w = wave + NW q: lane q tests word q's threshold (one
+      // LDS round trip for all of them), then only the flagged words run
+      const int nq = (Sw - wave + NW - 1) / NW;  // <= 64 (S <= 4096)
+      const int wl = wave + NW * lane;
+      const bool own = lane < nq;
+      const uint64_t oldb = own ? wbits[wl] : 0ull;
+      uint64_t need = __ballot(own && (!incremental || !(drift < (double)wthr[wl])));
+      while (need) {  // wave-uniform
+        const int q = __builtin_ctzll(need);
+        need &= need - 1;
+        const int w = wave + NW * q;
+        const int j = w * 64 + lane;
+        bool m = false;
+        float t = INFINITY;
+        if (j < S) {
+          double g;
+          m = member0_margin<KC>(cl, ys[j].x, ys[j].y, g);
+          t = (float)((drift + g * inv2c) * (1.0 - 0x1p-20));  // D + g / (2 Cmax), rounded down
+        }
+        t = wave_min_f(t);
+        const uint64_t bits = __ballot(m);
+        const uint64_t was = ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(oldb >> 32), q) << 32) |
+                             (unsigned)__builtin_amdgcn_readlane((int)oldb, q);
+        if (it == 0 || bits != was) chg = 1;
+        if (lane == 0) {
+          wbits[w] = bits;
+          wthr[w] = t;
+        }
+#if KML_STAMPS
+        if (tid == 0) km_acc[KS_WORDS] += 1;  // wave 0's words; x NW at the flush (an estimate)
+#endif
+      }
+    }
+    if (lane == 0) s_flag[1 + wave] = chg;
     __syncthreads();
-    const int n = wpos[kFusedMaxW];
-    if (tid < 2) {  // lane 0: real chain, lane 1: imaginary chain, ascending j
-      const double acc = ordered_sum(tid == 0 ? sr : si, reinterpret_cast<const double *>(ym) + tid, n);
+    int rebuild = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) rebuild |= s_flag[1 + w];
+    KM_STAMP(KS_ASSIGN);
+    if (rebuild) {  // member list changed: rebuild it
+      KM_COUNT(KS_COMPACTIONS, 1);
+      // every wave computes the word offsets itself (exclusive prefix of the
+      // popcounts, DPP scan over lanes = words, Sw <= 64) and scatters its own
+      // words' members: no barrier between the two
+      const uint64_t bl = lane < Sw ? wbits[lane] : 0ull;
+      const int c = __popcll(bl);
+      const int incl = wave_inclusive_scan_i(c);
+      const int excl = incl - c;
+      nmem = __builtin_amdgcn_readlane(incl, 63);
+      for (int w = wave; w < Sw; w += NW) {
+        const uint64_t bits = ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(bl >> 32), w) << 32) |
+                              (unsigned)__builtin_amdgcn_readlane((int)bl, w);
+        if ((bits >> lane) & 1) {
+          const int p = __builtin_amdgcn_readlane(excl, w) + __popcll(bits & ((1ull << lane) - 1));
+          mem[p] = (unsigned short)(w * 64 + lane);
+        }
+      }
+      __syncthreads();
+    }
+    KM_STAMP(KS_COMPACT);
+    const int n = nmem;
+    cnt += n;
+    if (scan) {  // wave 0: the real chain, wave 1: the imaginary chain (kFusedT = 128)
+      int steps = 0;
+      const double acc = ordered_sum_wave(wave == 0 ? sr : si, reinterpret_cast<const double *>(ys) + wave, mem, n, S,
+                                          lane, steps);
+      KM_COUNT(KS_STEPS, steps);
+      if (wave == 0) sr = acc;
+      if (wave == 1) {
+        si = acc;
+        if (lane == 0) red_d[0] = acc;
+      }
+      __syncthreads();
+      if (tid == 0) si = red_d[0];
+    } else if (tid < 2) {  // lane 0: real chain, lane 1: imaginary chain, ascending j
+      const double acc = ordered_sum(tid == 0 ? sr : si, reinterpret_cast<const double *>(ys) + tid, mem, n, S);
       const double other = __shfl_xor(acc, 1);
       sr = tid == 0 ? acc : other;
       si = tid == 0 ? other : acc;
-      cnt += n;
-      if (tid == 0) {
-        // convergence: every cluster equals the previous iteration's (kmeans.cc:47-56)
-        bool same = true;
-        for (int k = 0; k < KC && same; ++k) {
-          const cplx ck{cons[2 * k], cons[2 * k + 1]};
-          const cplx a = kml_cmul(ck, hat);
-          const cplx b = have_prev ? kml_cmul(ck, prev) : cplx{0.0, 0.0};
-          same = (a.re == b.re) && (a.im == b.im);
-        }
-        int done = 0;
-        if (same) {
-          done = 1;
-        } else {
-          prev = hat;
-          have_prev = true;
-          const cplx m0 = kml_cdiv(cplx{sr, si}, cplx{(double)cnt, 0.0});  // kmeans.cc:59-62
-          hat = kml_cdiv(m0, c0);                                         // kmeans.cc:64-71
-        }
-        s_hat = make_double2(hat.re, hat.im);
-        s_done = done;
-      }
+    }
+    KM_STAMP(KS_SUM);
+    if (tid == 0) {
+      const cplx m0 = cdiv_count(sr, si, cnt);  // kmeans.cc:59-62
+      const cplx nh = cdiv_const(m0, c0, c0k);  // kmeans.cc:64-71
+      s_hat = make_double2(nh.re, nh.im);
     }
     __syncthreads();
+    KM_STAMP(KS_UPDATE);
     hat = cplx{s_hat.x, s_hat.y};
-    if (s_done) break;
   }
+#if KML_STAMPS
+  if (tid == 0) {
+    km_acc[KS_WORDS] *= NW;
+    for (int i = 0; i <= KS_STEPS; ++i) atomicAdd(&kml_km_stamps[i], km_acc[i]);
+  }
+#endif
   if (tid == 0) {
     const cplx hh = kml_cdiv(kml_cmul(c0, hat), c0);  // simulator.cc:145
     h_hat[cw] = make_double2(hh.re, hh.im);
@@ -443,13 +873,18 @@ __global__ __launch_bounds__(kFusedT) void km_fused_kernel(const double *__restr
 template <int KC>
 bool run_kmeans_fused(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
                       double2 *h_hat, double2 *h4, hipStream_t s, hipError_t &err) {
-  const size_t lds = 2 * sizeof(double2) * (size_t)S;
+  const size_t lds = sizeof(double2) * (size_t)S + 2 * (size_t)((S + 24 + 7) & ~7);
   if (S > 64 * kFusedMaxW || lds > 128 * 1024) return false;
   if (const char *e = getenv("KML_KMEANS"))
     if (e[0] == 's') return false;  // KML_KMEANS=split: the two-launch form (A/B)
   err = hipFuncSetAttribute((const void *)km_fused_kernel<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return true;
-  hipLaunchKernelGGL(km_fused_kernel<KC>, dim3(B), dim3(kFusedT), lds, s, cons, rot, y, S, iters, h_hat, h4);
+  int incremental = 1;  // KML_KM_INCR=0: assign every word every iteration (A/B)
+  if (const char *e = getenv("KML_KM_INCR")) incremental = e[0] != '0';
+  int scan = 1;  // KML_KM_SCAN=0: the two-lane sequential sums (A/B)
+  if (const char *e = getenv("KML_KM_SCAN")) scan = e[0] != '0';
+  hipLaunchKernelGGL(km_fused_kernel<KC>, dim3(B), dim3(kFusedT), lds, s, cons, rot, y, S, iters, h_hat, h4,
+                     incremental, scan);
   err = hipGetLastError();
   return true;
 }
@@ -529,6 +964,15 @@ __global__ void div_probe_kernel(const double *in, int n, double *out) {
   o[7] = rcp_refine(s);
 }
 }  // namespace
+
+extern "C" int kml_debug_km_stamps(unsigned long long *out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(kml::kml_km_stamps), sizeof(kml::kml_km_stamps));
+  if (reset) {
+    unsigned long long zero[KS_SLOTS] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(kml::kml_km_stamps), zero, sizeof(zero));
+  }
+  return e == hipSuccess ? 0 : -3;
+}
 
 hipError_t launch_div_probe(const double *in, int n, double *out, hipStream_t s) {
   if (n == 0) return hipSuccess;

@@ -327,7 +327,9 @@ def test_fused_demap_matches_separate(data_dir, blind, monkeypatch):
 
 
 @pytest.mark.parametrize("matrix,modem,snr,n", [
-    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", 2.0, 200),
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", 2.0, 1000),
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", -1.0, 500),
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", 8.0, 300),
     ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", 5.01, 100),
     ("PEG2304regular0.5.txt", "4bit_16QAM_phi1.txt", 8.0, 50),
     ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", 6.77, 30),
