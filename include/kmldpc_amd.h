@@ -17,6 +17,11 @@
  *   kml_kmeans                kmldpc::KMeans(data, constellations, iter); Run(); clusters()
  *                                                                                  include/kmeans.h:14-22
  *                             + h_hat = clusters[0]/c[0] and its 4 rotations       src/simulator.cc:145-148
+ *   kml_kmeans_state          KMeans::clusters(), KMeans::idx() after Run()          include/kmeans.h:18-19
+ *                                                                                  (src/kmeans.cc:72-83, 86-94)
+ *   kml_kmeans_dump_mat       void KMeans::DumpToMat(std::string&, std::vector<complex>& append)
+ *                                                                                  include/kmeans.h:21, src/kmeans.cc:99-109
+ *                             (host only; the reference needs matio, this writes the level-5 file itself)
  *   kml_decode_frames         void KmCodec::Decoder(ModemLinearSystem&, const std::vector<complex>& h_hats, int *uu_hat)
  *                                                                                  include/kmcodec.h:23-25
  *   kml_decode_candidates     the same KmCodec::Decoder with the caller's h_hats (any 1..4 estimates)
@@ -123,6 +128,21 @@ int kml_demap(kml_ctx *ctx, const double *y, const double *h, double var, int B,
 /* KMeans(y, constellation, iters).Run(); h_hat = clusters[0]/c[0];
  * h4[j] = h_hat * exp(i*kPi/2*j).  h_hat[B][2], h4[B][4][2] (either may be NULL). */
 int kml_kmeans(kml_ctx *ctx, const double *y, int B, int iters, double *h_hat, double *h4, int flags);
+
+/* The same Run, then KMeans::clusters() = c[k] * hatH -> clusters[B][Kc][2] and
+ * KMeans::idx() (the closing assignment, first minimum of glibc hypot,
+ * kmeans.cc:76-83) -> idx[B][S].  Either output may be NULL. */
+int kml_kmeans_state(kml_ctx *ctx, const double *y, int B, int iters, double *clusters, int32_t *idx, int flags);
+
+/* KMeans::DumpToMat(filename, append) of ONE codeword (host only, no context):
+ * a MAT-file level 5 with the reference's variables, each an n x 1 column,
+ * uncompressed as lab::Mat writes them (lib/lab/src/mat.cc): data[S] complex,
+ * cluster[Kc] complex, idx[S] int32, constellations[Kc] complex, hHats =
+ * append[0..3] complex, realH = append[4] (1 x 1 complex).  Complex inputs
+ * are interleaved (re, im); append holds 5 complex values.  Returns 0,
+ * KML_E_ARG or KML_E_IO. */
+int kml_kmeans_dump_mat(const char *path, const double *data, int S, const double *clusters, const int32_t *idx,
+                        const double *constellations, int Kc, const double *append);
 
 /* KmCodec::Decoder for B codewords at Es/N0 = snr dB.  true_h[B][2] selects
  * the known-channel path ([decoder] true_h_arg = true); true_h == NULL runs the

@@ -16,6 +16,8 @@
 //                                    simulator's `KmCodec` type becomes `GpuKmCodec` at its use sites)
 //   gpu_kmeans_h_hats     KMeans(received, constellations, 20).Run(); clusters()[0] / c[0] and its
 //                         4 rotations (include/kmeans.h:14-22, src/simulator.cc:136-148)
+//   GpuKMeans             the kmldpc::KMeans interface (include/kmeans.h:12-32): Run, clusters,
+//                         idx and DumpToMat (which the reference only has with matio)
 #ifndef KMLDPC_AMD_GPU_CODECS_HPP
 #define KMLDPC_AMD_GPU_CODECS_HPP
 
@@ -165,6 +167,39 @@ inline std::vector<std::complex<double>> gpu_kmeans_h_hats(kml_ctx *ctx, const s
                         reinterpret_cast<double *>(h4.data()), 0));
   return h4;
 }
+
+// kmldpc::KMeans with the same calls (include/kmeans.h:14-22): the context's
+// constellation is the one the reference passes in (mls.constellations()).
+class GpuKMeans {
+ public:
+  GpuKMeans(kml_ctx *ctx, std::vector<std::complex<double>> &data, std::vector<std::complex<double>> &constellations,
+            int iter)
+      : ctx_(ctx), data_(data), constellations_(constellations), iter_(iter),
+        clusters_(constellations.size()), idx_(data.size()) {}
+  void Run() {
+    check(ctx_, kml_kmeans_state(ctx_, reinterpret_cast<const double *>(data_.data()), 1, iter_,
+                                 reinterpret_cast<double *>(clusters_.data()), idx_.data(), 0));
+  }
+  std::vector<std::complex<double>> clusters() { return clusters_; }
+  std::vector<int> idx() { return std::vector<int>(idx_.begin(), idx_.end()); }
+  // KMeans::DumpToMat (src/kmeans.cc:99-109): append = the 4 candidates + the true H
+  void DumpToMat(std::string &filename, std::vector<std::complex<double>> &append) {
+    if (append.size() < 5 ||
+        kml_kmeans_dump_mat(filename.c_str(), reinterpret_cast<const double *>(data_.data()), (int)data_.size(),
+                            reinterpret_cast<const double *>(clusters_.data()), idx_.data(),
+                            reinterpret_cast<const double *>(constellations_.data()), (int)constellations_.size(),
+                            reinterpret_cast<const double *>(append.data())) != KML_OK) {
+      lab::logger::ERROR("Creating file failed, file name is " + filename, true);  // lab/src/mat.cc:21-24
+      exit(-1);
+    }
+  }
+
+ private:
+  kml_ctx *ctx_;
+  std::vector<std::complex<double>> data_, constellations_, clusters_;
+  std::vector<int32_t> idx_;
+  int iter_;
+};
 
 }  // namespace kml_lab
 

@@ -22,7 +22,7 @@ import os
 
 import numpy as np
 
-__all__ = ["Context", "KmlError", "lib", "LIB_PATH", "BinaryLDPCCodec", "KMeans", "KmCodec"]
+__all__ = ["Context", "KmlError", "lib", "LIB_PATH", "BinaryLDPCCodec", "KMeans", "KmCodec", "dump_kmeans_mat"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KML_LIB") or os.path.join(HERE, "libkmldpc_amd.so")  # KML_LIB: A/B builds
@@ -79,6 +79,8 @@ def lib():
         "kml_bp_decode": (I, [P, P, I, I, P, P, P, P, I]),
         "kml_demap": (I, [P, P, P, D, I, P, I]),
         "kml_kmeans": (I, [P, P, I, I, P, P, I]),
+        "kml_kmeans_state": (I, [P, P, I, I, P, P, I]),
+        "kml_kmeans_dump_mat": (I, [C.c_char_p, P, I, P, P, P, I, P]),
         "kml_decode_frames": (I, [P, P, P, D, I, P, P, P, P, P, I]),
         "kml_count_errors": (I, [P, P, P, I, P, I]),
         "kml_decode_candidates": (I, [P, P, P, I, D, I, P, P, P, P, I]),
@@ -242,6 +244,15 @@ class Context:
         h4 = np.zeros((B, 4, 2))
         self._chk(lib().kml_kmeans(self._h, _p(y), B, int(iters), _p(hh), _p(h4), 0), "kml_kmeans")
         return hh, h4
+
+    def kmeans_state(self, y, iters=20):
+        """KMeans(y, constellations, iters).Run(); clusters() -> [B, Kc, 2], idx() -> [B, S] int32."""
+        y = _f64(y).reshape(-1, self.S, 2)
+        B = y.shape[0]
+        cl = np.zeros((B, self.Kc, 2))
+        idx = np.zeros((B, self.S), np.int32)
+        self._chk(lib().kml_kmeans_state(self._h, _p(y), B, int(iters), _p(cl), _p(idx), 0), "kml_kmeans_state")
+        return cl, idx
 
     def decode_frames(self, y, snr, true_h=None, histogram=False):
         """KmCodec::Decoder: known channel if true_h is given, else the blind path.
@@ -545,6 +556,46 @@ class KMeans:
     def h_hats(self):
         """the 4 phase candidates (src/simulator.cc:146-148)."""
         return self._h4
+
+    def clusters(self):
+        """KMeans::clusters() per codeword, [B, Kc, 2] (include/kmeans.h:18)."""
+        self._state()
+        return self._cl
+
+    def idx(self):
+        """KMeans::idx() per codeword, [B, S] int32 (include/kmeans.h:19)."""
+        self._state()
+        return self._idx
+
+    def _state(self):
+        if getattr(self, "_cl", None) is None:
+            self._cl, self._idx = self.ctx.kmeans_state(self.data, self.iters)
+
+    def DumpToMat(self, filename, append, b=0):
+        """KMeans::DumpToMat (src/kmeans.cc:99-109) of codeword b: append = the 4
+        candidates and the true H (5 complex values, [5, 2] or complex[5])."""
+        self._state()
+        dump_kmeans_mat(filename, np.asarray(self.data).reshape(-1, self.ctx.S, 2)[b], self._cl[b], self._idx[b],
+                        self.ctx.constellation(), append)
+
+
+def dump_kmeans_mat(filename, data, clusters, idx, constellations, append):
+    """kml_kmeans_dump_mat: one codeword's k-means state as a MAT-file level 5
+    (data, cluster, idx, constellations, hHats, realH; lib/lab/src/mat.cc)."""
+    def cplx(a, n=None):
+        a = np.asarray(a)
+        if np.iscomplexobj(a):
+            a = np.stack([a.real, a.imag], -1)
+        a = np.ascontiguousarray(a, np.float64).reshape(-1, 2)
+        assert n is None or a.shape[0] == n
+        return a
+    d, c, k = cplx(data), cplx(clusters), cplx(constellations)
+    ap = cplx(append, 5)
+    ix = np.ascontiguousarray(idx, np.int32).reshape(-1)
+    assert ix.size == d.shape[0] and c.shape[0] == k.shape[0]
+    rc = lib().kml_kmeans_dump_mat(os.fsencode(filename), _p(d), d.shape[0], _p(c), _p(ix), _p(k), k.shape[0], _p(ap))
+    if rc != 0:
+        raise KmlError(f"kml_kmeans_dump_mat: error {rc}")
 
 
 class KmCodec:

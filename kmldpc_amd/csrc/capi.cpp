@@ -1009,6 +1009,112 @@ int kml_kmeans(kml_ctx *c, const double *y, int B, int iters, double *h_hat, dou
   return sync(c);
 }
 
+int kml_kmeans_state(kml_ctx *c, const double *y, int B, int iters, double *clusters, int32_t *idx, int flags) {
+  if (!c || !y || B < 0 || iters < 0) return fail(c, KML_E_ARG, "kml_kmeans_state: bad argument");
+  if (B == 0) return KML_OK;
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const int S = c->code.cc_len / c->modem.bits;
+  const int Kc = c->modem.Kc;
+  const double *d_y;
+  TRY(stage_in(c, c->w_y, y, (size_t)B * S * 2, flags, d_y));
+  HIPCHK(c, c->w_hhat.ensure(sizeof(double2) * B), "hipMalloc");
+  HIPCHK(c, c->w_h4.ensure(sizeof(double2) * 4 * B), "hipMalloc");
+  HIPCHK(c, c->w_h.ensure(sizeof(double2) * B), "hipMalloc");  // the final hatH
+  double *d_cl;
+  int32_t *d_idx;
+  TRY(stage_out_ptr(c, c->w_met, clusters, (size_t)B * Kc * 2, flags, d_cl));
+  TRY(stage_out_ptr(c, c->w_cwerr, idx, (size_t)B * S, flags, d_idx));
+  const double *cons = c->d_cons.as<double>();
+  HIPCHK(c, c->w_km.ensure(kml::kmeans_workspace_bytes(S, B)), "hipMalloc(kmeans)");
+  Timer t(c, "kmeans", -1, (double)B * S * 16.0);
+  HIPCHK(c, kml::launch_kmeans(Kc, cons, cons + c->modem.pts.size(), reinterpret_cast<const double2 *>(d_y), S, iters, B,
+                               c->w_hhat.as<double2>(), c->w_h4.as<double2>(), c->w_km.p, c->stream,
+                               c->w_h.as<double2>()),
+         "kmeans");
+  t.stop();
+  HIPCHK(c, kml::launch_kmeans_state(Kc, cons, reinterpret_cast<const double2 *>(d_y), S, B, c->w_h.as<double2>(),
+                                     reinterpret_cast<double2 *>(d_cl), d_idx, c->stream),
+         "kmeans_state");
+  TRY(copy_out(c, clusters, (const double *)d_cl, (size_t)B * Kc * 2, flags));
+  TRY(copy_out(c, idx, (const int32_t *)d_idx, (size_t)B * S, flags));
+  return sync(c);
+}
+
+// ---- MAT-file level 5 writer (KMeans::DumpToMat, src/kmeans.cc:99-109) ----
+// What lab::Mat does through matio (lib/lab/src/mat.cc): Mat_CreateVer(...,
+// MAT_FT_DEFAULT) = a level-5 file, each variable written uncompressed
+// (MAT_COMPRESSION_NONE) as an n x 1 column: WriteVector(complex) ->
+// mxDOUBLE_CLASS with the complex flag (real part, then imaginary part),
+// WriteVector(int32) -> mxINT32_CLASS, WriteComplex -> a 1 x 1 complex double.
+namespace {
+struct MatOut {
+  std::string buf;
+  void raw(const void *p, size_t n) { buf.append(static_cast<const char *>(p), n); }
+  void u32(uint32_t v) { raw(&v, 4); }
+  void pad8() {
+    while (buf.size() % 8) buf.push_back('\0');
+  }
+  // one data element: tag (type, bytes) + data, padded to 8 bytes
+  void element(uint32_t type, const void *p, size_t n) {
+    u32(type);
+    u32((uint32_t)n);
+    raw(p, n);
+    pad8();
+  }
+  enum { miINT8 = 1, miINT32 = 5, miUINT32 = 6, miDOUBLE = 9, miMATRIX = 14 };
+  enum { mxDOUBLE_CLASS = 6, mxINT32_CLASS = 12 };
+  void matrix(const char *name, uint32_t cls, bool cplx, int rows, const void *re, const void *im, size_t elem) {
+    MatOut body;
+    const uint32_t flags[2] = {cls | (cplx ? 0x0800u : 0u), 0u};
+    body.element(miUINT32, flags, sizeof(flags));
+    const int32_t dims[2] = {rows, 1};
+    body.element(miINT32, dims, sizeof(dims));
+    body.element(miINT8, name, strlen(name));
+    const uint32_t t = cls == mxINT32_CLASS ? miINT32 : miDOUBLE;
+    body.element(t, re, (size_t)rows * elem);
+    if (cplx) body.element(t, im, (size_t)rows * elem);
+    u32(miMATRIX);
+    u32((uint32_t)body.buf.size());
+    raw(body.buf.data(), body.buf.size());
+  }
+  void complex_vec(const char *name, const double *z, int n) {  // z interleaved (re, im)
+    std::vector<double> re(n), im(n);
+    for (int i = 0; i < n; ++i) {
+      re[i] = z[2 * i];
+      im[i] = z[2 * i + 1];
+    }
+    matrix(name, mxDOUBLE_CLASS, true, n, re.data(), im.data(), sizeof(double));
+  }
+};
+}  // namespace
+
+int kml_kmeans_dump_mat(const char *path, const double *data, int S, const double *clusters, const int32_t *idx,
+                        const double *constellations, int Kc, const double *append) {
+  if (!path || !data || !clusters || !idx || !constellations || !append || S < 0 || Kc < 0) return KML_E_ARG;
+  MatOut m;
+  char hdr[128];
+  memset(hdr, ' ', sizeof(hdr));
+  const char *text = "MATLAB 5.0 MAT-file, Platform: GLNXA64, Created by: kmldpc_amd (KMeans::DumpToMat)";
+  memcpy(hdr, text, strlen(text));
+  memset(hdr + 116, 0, 8);  // subsystem data offset: none
+  const uint16_t ver = 0x0100;
+  memcpy(hdr + 124, &ver, 2);
+  hdr[126] = 'I';  // written little-endian: reads back as "IM"
+  hdr[127] = 'M';
+  m.raw(hdr, sizeof(hdr));
+  m.complex_vec("data", data, S);
+  m.complex_vec("cluster", clusters, Kc);
+  m.matrix("idx", MatOut::mxINT32_CLASS, false, S, idx, nullptr, sizeof(int32_t));
+  m.complex_vec("constellations", constellations, Kc);
+  m.complex_vec("hHats", append, 4);   // append[0..3]
+  m.complex_vec("realH", append + 8, 1);  // append[4] (WriteComplex: 1 x 1)
+  FILE *f = fopen(path, "wb");
+  if (!f) return KML_E_IO;
+  const bool ok = fwrite(m.buf.data(), 1, m.buf.size(), f) == m.buf.size();
+  return (fclose(f) == 0 && ok) ? KML_OK : KML_E_IO;
+}
+
 int kml_decode_frames(kml_ctx *c, const double *y, const double *true_h, double snr, int B, uint8_t *uu_hat,
                       int32_t *chosen, double *metrics, int32_t *ret, double *h_hat, int flags) {
   if (!c || !y || !uu_hat || B < 0) return fail(c, KML_E_ARG, "kml_decode_frames: bad argument");

@@ -152,8 +152,12 @@ struct KmState {
   int cnt, it, done, have_prev;
 };
 size_t kmeans_workspace_bytes(int S, int B);
+// hat_out (optional): the final hatH per codeword (clusters_ = c[k] * hatH).
 hipError_t launch_kmeans(int Kc, const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
-                         double2 *h_hat, double2 *h4, void *ws, hipStream_t s);
+                         double2 *h_hat, double2 *h4, void *ws, hipStream_t s, double2 *hat_out = nullptr);
+// KMeans::clusters() / idx() from the final hatH (kmeans.cc:72-83): clusters[B][Kc], idx[B][S] (either may be null).
+hipError_t launch_kmeans_state(int Kc, const double *cons, const double2 *y, int S, int B, const double2 *hat,
+                               double2 *clusters, int *idx, hipStream_t s);
 
 // GPU frame generation (counter-based Philox; statistically equivalent to the
 // reference's sequential Park-Miller stream, not bit-equal).

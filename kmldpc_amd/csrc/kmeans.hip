@@ -233,9 +233,10 @@ __global__ void km_update_kernel(const double *__restrict__ cons, const double2 
 
 __global__ void km_final_kernel(const double *__restrict__ cons, const double *__restrict__ rot, int B,
                                 const KmState *__restrict__ st, double2 *__restrict__ h_hat,
-                                double2 *__restrict__ h4) {
+                                double2 *__restrict__ h4, double2 *__restrict__ hat_out) {
   const int cw = blockIdx.x * blockDim.x + threadIdx.x;
   if (cw >= B) return;
+  if (hat_out) hat_out[cw] = st[cw].hat;
   const cplx c0{cons[0], cons[1]};
   const cplx hat{st[cw].hat.x, st[cw].hat.y};
   const cplx hh = kml_cdiv(kml_cmul(c0, hat), c0);  // simulator.cc:145
@@ -634,7 +635,7 @@ __global__ __launch_bounds__(kFusedT) void km_fused_kernel(const double *__restr
                                                            const double *__restrict__ rot,
                                                            const double2 *__restrict__ y, int S, int iters,
                                                            double2 *__restrict__ h_hat, double2 *__restrict__ h4,
-                                                           int incremental, int scan) {
+                                                           double2 *__restrict__ hat_out, int incremental, int scan) {
   extern __shared__ __attribute__((aligned(16))) unsigned char kmem[];
   double2 *ys = reinterpret_cast<double2 *>(kmem);  // [S] symbols
   // compacted cluster-0 member indices, ascending: [S + 24], 16-byte aligned
@@ -861,6 +862,7 @@ __global__ __launch_bounds__(kFusedT) void km_fused_kernel(const double *__restr
   }
 #endif
   if (tid == 0) {
+    if (hat_out) hat_out[cw] = make_double2(hat.re, hat.im);  // the final hatH (clusters_ = c[k] * hatH)
     const cplx hh = kml_cdiv(kml_cmul(c0, hat), c0);  // simulator.cc:145
     h_hat[cw] = make_double2(hh.re, hh.im);
     for (int j = 0; j < 4; ++j) {  // simulator.cc:146-148
@@ -872,7 +874,7 @@ __global__ __launch_bounds__(kFusedT) void km_fused_kernel(const double *__restr
 
 template <int KC>
 bool run_kmeans_fused(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
-                      double2 *h_hat, double2 *h4, hipStream_t s, hipError_t &err) {
+                      double2 *h_hat, double2 *h4, double2 *hat_out, hipStream_t s, hipError_t &err) {
   const size_t lds = sizeof(double2) * (size_t)S + 2 * (size_t)((S + 24 + 7) & ~7);
   if (S > 64 * kFusedMaxW || lds > 128 * 1024) return false;
   if (const char *e = getenv("KML_KMEANS"))
@@ -883,7 +885,7 @@ bool run_kmeans_fused(const double *cons, const double *rot, const double2 *y, i
   if (const char *e = getenv("KML_KM_INCR")) incremental = e[0] != '0';
   int scan = 1;  // KML_KM_SCAN=0: the two-lane sequential sums (A/B)
   if (const char *e = getenv("KML_KM_SCAN")) scan = e[0] != '0';
-  hipLaunchKernelGGL(km_fused_kernel<KC>, dim3(B), dim3(kFusedT), lds, s, cons, rot, y, S, iters, h_hat, h4,
+  hipLaunchKernelGGL(km_fused_kernel<KC>, dim3(B), dim3(kFusedT), lds, s, cons, rot, y, S, iters, h_hat, h4, hat_out,
                      incremental, scan);
   err = hipGetLastError();
   return true;
@@ -891,9 +893,9 @@ bool run_kmeans_fused(const double *cons, const double *rot, const double2 *y, i
 
 template <int KC>
 hipError_t run_kmeans(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
-                      KmState *st, uint64_t *mem, double2 *h_hat, double2 *h4, hipStream_t s) {
+                      KmState *st, uint64_t *mem, double2 *h_hat, double2 *h4, double2 *hat_out, hipStream_t s) {
   hipError_t ferr = hipSuccess;
-  if (run_kmeans_fused<KC>(cons, rot, y, S, iters, B, h_hat, h4, s, ferr)) return ferr;
+  if (run_kmeans_fused<KC>(cons, rot, y, S, iters, B, h_hat, h4, hat_out, s, ferr)) return ferr;
   const int Sw = (S + 63) / 64;
   const dim3 lanes((B + 63) / 64), l64(64);
   hipLaunchKernelGGL(km_init_kernel, lanes, l64, 0, s, cons, y, S, B, st);
@@ -902,7 +904,7 @@ hipError_t run_kmeans(const double *cons, const double *rot, const double2 *y, i
     hipLaunchKernelGGL(km_assign_kernel<KC>, dim3(B), dim3(threads), 0, s, cons, y, S, Sw, st, mem);
     hipLaunchKernelGGL(km_update_kernel<KC>, lanes, l64, 0, s, cons, y, S, Sw, iters, B, st, mem);
   }
-  hipLaunchKernelGGL(km_final_kernel, lanes, l64, 0, s, cons, rot, B, st, h_hat, h4);
+  hipLaunchKernelGGL(km_final_kernel, lanes, l64, 0, s, cons, rot, B, st, h_hat, h4, hat_out);
   return hipGetLastError();
 }
 
@@ -913,18 +915,108 @@ size_t kmeans_workspace_bytes(int S, int B) {
 }
 
 hipError_t launch_kmeans(int Kc, const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
-                         double2 *h_hat, double2 *h4, void *ws, hipStream_t s) {
+                         double2 *h_hat, double2 *h4, void *ws, hipStream_t s, double2 *hat_out) {
   if (B == 0) return hipSuccess;
   KmState *st = reinterpret_cast<KmState *>(ws);
   uint64_t *mem = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(ws) + (size_t)B * sizeof(KmState));
   switch (Kc) {
-    case 2: return run_kmeans<2>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, s);
-    case 4: return run_kmeans<4>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, s);
-    case 8: return run_kmeans<8>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, s);
-    case 16: return run_kmeans<16>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, s);
-    case 64: return run_kmeans<64>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, s);
+    case 2: return run_kmeans<2>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, hat_out, s);
+    case 4: return run_kmeans<4>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, hat_out, s);
+    case 8: return run_kmeans<8>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, hat_out, s);
+    case 16: return run_kmeans<16>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, hat_out, s);
+    case 64: return run_kmeans<64>(cons, rot, y, S, iters, B, st, mem, h_hat, h4, hat_out, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+// KMeans::clusters() and idx() after Run (include/kmeans.h:18-19): the final
+// clusters_ = c[k] * hatH and the closing assignment loop (kmeans.cc:76-83),
+// idx_[i] = the FIRST k minimising glibc hypot(clusters_[k] - data_[i]).  The
+// simulator computes idx and drops it (simulator.cc:142); it is what
+// KMeans::DumpToMat writes (kmeans.cc:99-109).  One thread per symbol; the
+// squared-norm screen of member0 with the exact hypot decision inside the tie
+// band, the reference loop for non-finite / extreme values.
+namespace {
+template <int KC>
+__device__ int first_argmin(const double2 *cl, double yr, double yi) {
+  double dm = 0.0;
+  int km = 0;
+  bool fin = true;
+  for (int k = 0; k < KC; ++k) {
+    const double dr = cl[k].x - yr, di = cl[k].y - yi;
+    const double d = dr * dr + di * di;
+    if (k == 0 || d < dm) {
+      dm = d;
+      km = k;
+    }
+    fin = fin && d2_ok(d);
+  }
+  if (fin) {
+    int ties = 0;
+    for (int k = 0; k < KC; ++k) {
+      const double dr = cl[k].x - yr, di = cl[k].y - yi;
+      ties += (dr * dr + di * di <= dm * (1.0 + kTieBand)) ? 1 : 0;
+    }
+    if (ties == 1) return km;  // every other squared distance is > dm (1 + 1e-12): hypot orders them alike
+    double hb = 0.0;
+    int kb = -1;
+    for (int k = 0; k < KC; ++k) {  // the band's contenders, exactly, first minimum
+      const double dr = cl[k].x - yr, di = cl[k].y - yi;
+      if (dr * dr + di * di <= dm * (1.0 + kTieBand)) {
+        const double h = kml_hypot(dr, di);
+        if (kb < 0 || h < hb) {
+          hb = h;
+          kb = k;
+        }
+      }
+    }
+    return kb;
+  }
+  double hb = kml_hypot(cl[0].x - yr, cl[0].y - yi);  // the reference loop
+  int kb = 0;
+  for (int k = 1; k < KC; ++k) {
+    const double h = kml_hypot(cl[k].x - yr, cl[k].y - yi);
+    if (h < hb) {
+      hb = h;
+      kb = k;
+    }
+  }
+  return kb;
+}
+
+template <int KC>
+__global__ __launch_bounds__(256) void km_state_kernel(const double *__restrict__ cons, const double2 *__restrict__ y,
+                                                       int S, const double2 *__restrict__ hat,
+                                                       double2 *__restrict__ clusters, int *__restrict__ idx) {
+  __shared__ double2 cl[KC];
+  const int cw = blockIdx.y;
+  const cplx h{hat[cw].x, hat[cw].y};
+  for (int k = threadIdx.x; k < KC; k += blockDim.x) {
+    const cplx p = kml_cmul(cplx{cons[2 * k], cons[2 * k + 1]}, h);  // kmeans.cc:72-74
+    cl[k] = make_double2(p.re, p.im);
+    if (blockIdx.x == 0 && clusters) clusters[(long long)cw * KC + k] = cl[k];
+  }
+  __syncthreads();
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= S || !idx) return;
+  const double2 v = y[(long long)cw * S + j];
+  idx[(long long)cw * S + j] = first_argmin<KC>(cl, v.x, v.y);
+}
+}  // namespace
+
+hipError_t launch_kmeans_state(int Kc, const double *cons, const double2 *y, int S, int B, const double2 *hat,
+                               double2 *clusters, int *idx, hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  const dim3 grid((S + 255) / 256, B), blk(256);
+  switch (Kc) {
+    case 2: hipLaunchKernelGGL(km_state_kernel<2>, grid, blk, 0, s, cons, y, S, hat, clusters, idx); break;
+    case 4: hipLaunchKernelGGL(km_state_kernel<4>, grid, blk, 0, s, cons, y, S, hat, clusters, idx); break;
+    case 8: hipLaunchKernelGGL(km_state_kernel<8>, grid, blk, 0, s, cons, y, S, hat, clusters, idx); break;
+    case 16: hipLaunchKernelGGL(km_state_kernel<16>, grid, blk, 0, s, cons, y, S, hat, clusters, idx); break;
+    case 64: hipLaunchKernelGGL(km_state_kernel<64>, grid, blk, 0, s, cons, y, S, hat, clusters, idx); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 // Probe for the device restatements of hypot / complex division / exp (tests).

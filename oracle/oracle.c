@@ -582,7 +582,11 @@ void orc_cdiv(double a, double b, double c, double d, double *re, double *im) {
 
 double orc_hypot(double x, double y) { return hypot(x, y); }
 
-void orc_kmeans_hhat(const double *y, int S, const double *cons, int Kc, int iters, double *h_hat) {
+/* KMeans::Run (src/kmeans.cc:15-84).  h_hat (optional) = clusters[0]/c[0]
+ * (simulator.cc:145); clusters (optional, [Kc] interleaved) = KMeans::clusters();
+ * idx (optional, [S]) = KMeans::idx(), the closing assignment (kmeans.cc:76-83). */
+void orc_kmeans_state(const double *y, int S, const double *cons, int Kc, int iters, double *h_hat, double *clusters,
+                      int *idx) {
   /* kmeans.cc:17-22: first max of |y| */
   int maxIndex = 0;
   double best = hypot(y[0], y[1]);
@@ -628,14 +632,33 @@ void orc_kmeans_hhat(const double *y, int S, const double *cons, int Kc, int ite
     hatH = cl[0] / c0;
     for (int k = 0; k < Kc; k++) cl[k] = CMPLX(cons[2 * k], cons[2 * k + 1]) * hatH;
   }
-  double complex hh = cl[0] / c0; /* simulator.cc:145 */
-  h_hat[0] = creal(hh);
-  h_hat[1] = cimag(hh);
+  if (h_hat) {
+    double complex hh = cl[0] / c0; /* simulator.cc:145 */
+    h_hat[0] = creal(hh);
+    h_hat[1] = cimag(hh);
+  }
+  if (clusters)
+    for (int k = 0; k < Kc; k++) {
+      clusters[2 * k] = creal(cl[k]);
+      clusters[2 * k + 1] = cimag(cl[k]);
+    }
+  if (idx) /* kmeans.cc:76-83: min_element = the first minimum */
+    for (int j = 0; j < S; j++) {
+      for (int k = 0; k < Kc; k++) dist[k] = hypot(creal(cl[k]) - y[2 * j], cimag(cl[k]) - y[2 * j + 1]);
+      int mi = 0;
+      for (int k = 1; k < Kc; k++)
+        if (dist[k] < dist[mi]) mi = k;
+      idx[j] = mi;
+    }
   free(cl);
   free(tmp);
   free(cnt);
   free(sum);
   free(dist);
+}
+
+void orc_kmeans_hhat(const double *y, int S, const double *cons, int Kc, int iters, double *h_hat) {
+  orc_kmeans_state(y, S, cons, Kc, iters, h_hat, NULL, NULL);
 }
 
 void orc_rotations(const double *h_hat, double *h4) {

@@ -65,6 +65,8 @@ void orc_demap(const orc_modem *m, const double *y, int S, double hr, double hi,
 /* --- k-means: src/kmeans.cc:15-84 (with its cumulative-count semantics),
  * followed by h_hat = clusters[0]/c[0] (src/simulator.cc:145). */
 void orc_kmeans_hhat(const double *y, int S, const double *cons, int Kc, int iters, double *h_hat);
+void orc_kmeans_state(const double *y, int S, const double *cons, int Kc, int iters, double *h_hat, double *clusters,
+                      int *idx);
 /* candidates h_hat*exp(i*kPi/2*j), j=0..3 (src/simulator.cc:146-148) */
 void orc_rotations(const double *h_hat, double *h4);
 

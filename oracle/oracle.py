@@ -43,6 +43,7 @@ def lib():
         L.orc_map.argtypes = [P, P, I, P]
         L.orc_demap.argtypes = [P, P, I, D, D, D, P]
         L.orc_kmeans_hhat.argtypes = [P, I, P, I, I, P]
+        L.orc_kmeans_state.argtypes = [P, I, P, I, I, P, P, P]
         L.orc_rotations.argtypes = [P, P]
         L.orc_rng_seed.argtypes = [P, C.c_long]
         L.orc_uniform.restype = D
@@ -147,6 +148,16 @@ def kmeans_hhat(y, cons, iters=20):
     out = np.zeros(2)
     lib().orc_kmeans_hhat(_p(y), y.size // 2, _p(cons), cons.size // 2, iters, _p(out))
     return out
+
+
+def kmeans_state(y, cons, iters=20):
+    """KMeans::clusters() [Kc, 2] and idx() [S] after Run (kmeans.cc:72-83)."""
+    y = np.ascontiguousarray(y, np.float64).reshape(-1)
+    cons = np.ascontiguousarray(cons, np.float64).reshape(-1)
+    cl = np.zeros(cons.size)
+    idx = np.zeros(y.size // 2, np.int32)
+    lib().orc_kmeans_state(_p(y), y.size // 2, _p(cons), cons.size // 2, iters, None, _p(cl), _p(idx))
+    return cl.reshape(-1, 2), idx
 
 
 def rotations(hh):

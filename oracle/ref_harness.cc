@@ -46,7 +46,7 @@ static void put_bits(FILE *f, const int *v, int n) {
 int main(int argc, char **argv) {
   if (argc < 5) {
     fprintf(stderr, "usage: %s config.toml snr n_codewords out.bin [mode]\n", argv[0]);
-    fprintf(stderr, "  mode: frames (default) | simulate | soft | softhist | rng\n");
+    fprintf(stderr, "  mode: frames (default) | simulate | soft | softhist | rng | kmstate\n");
     return 2;
   }
   const std::string cfg = argv[1];
@@ -183,6 +183,43 @@ int main(int argc, char **argv) {
     put_f64(f, ssink.fer());
     for (int32_t e : cw_errs) put_i32(f, e);
     fclose(f);
+    return 0;
+  }
+
+  if (mode == "kmstate") {
+    // KMeans::clusters() and KMeans::idx() after Run (include/kmeans.h:18-19)
+    // on the simulator's frames (simulator.cc:116-142): per codeword y,
+    // clusters[Kc], idx[S].
+    std::vector<int> uu(K), cc(N);
+    for (int i = 0; i < ncw; i++) {
+      lab::SourceSink ssink;
+      ssink.GetBitStr(uu.data(), K);
+      codec.Encoder(uu.data(), cc.data());
+      std::complex<double> true_h;
+      lab::CLCRandNum::Get().Normal(true_h);
+      true_h *= sqrt(0.5);
+      std::vector<std::complex<double>> gh(1, true_h);
+      mls.PartitionModemLSystem(cc.data(), gh);
+      auto constellations = mls.constellations();
+      auto received = mls.GetRecvSymbol();
+      kmldpc::KMeans km(received, constellations, 20);
+      km.Run();
+      auto cl = km.clusters();
+      auto idx = km.idx();
+      put_f64(f, true_h.real());
+      put_f64(f, true_h.imag());
+      for (auto &v : received) {
+        put_f64(f, v.real());
+        put_f64(f, v.imag());
+      }
+      for (auto &v : cl) {
+        put_f64(f, v.real());
+        put_f64(f, v.imag());
+      }
+      for (int v : idx) put_i32(f, v);
+    }
+    fclose(f);
+    delete direct;
     return 0;
   }
 

@@ -68,7 +68,8 @@ int main(int argc, char **argv) {
   lab::SourceSink ssink;
   std::vector<int> uu(K), cc(N), uu_ref(K), uu_gpu(K), b_ref(K), b_gpu(K);
   std::vector<double> bit_in(N, 0.5), m2v(N);
-  int mm_km = 0, mm_bp_ret = 0, mm_bp_uu = 0, mm_bp_cc = 0, mm_bp_syn = 0, mm_cand = 0, err_ref = 0, err_gpu = 0;
+  int mm_km = 0, mm_bp_ret = 0, mm_bp_uu = 0, mm_bp_cc = 0, mm_bp_syn = 0, mm_cand = 0, mm_kmstate = 0, err_ref = 0,
+      err_gpu = 0;
   for (int i = 0; i < ncw; i++) {
     ssink.GetBitStr(uu.data(), K);
     ref_km.Encoder(uu.data(), cc.data());
@@ -90,6 +91,16 @@ int main(int argc, char **argv) {
       for (size_t j = 0; j < 4; j++) h_hats.push_back(h_hat * exp(std::complex<double>(0, (lab::kPi / 2) * j)));
       auto g4 = kml_lab::gpu_kmeans_h_hats(gpu_km.context(), mls.GetRecvSymbol());
       if (memcmp(g4.data(), h_hats.data(), sizeof(double) * 8) != 0) mm_cand++;
+      kml_lab::GpuKMeans gkm(gpu_km.context(), received, constellations, 20);
+      gkm.Run();
+      auto gcl = gkm.clusters();
+      if (gcl != cl || gkm.idx() != km.idx()) mm_kmstate++;
+      if (i == 0) {  // KMeans::DumpToMat of the first codeword (append = candidates + true H)
+        std::string fn = "kmeans0.mat";
+        std::vector<std::complex<double>> app(h_hats);
+        app.push_back(true_h);
+        gkm.DumpToMat(fn, app);
+      }
     }
     // the whole receive step
     ref_km.Decoder(mls, h_hats, uu_ref.data());
@@ -111,8 +122,9 @@ int main(int argc, char **argv) {
   }
   printf("{\"codewords\": %d, \"K\": %d, \"known\": %d, \"is5g\": %d, \"kmcodec_uu_mismatch\": %d, "
          "\"candidate_mismatch\": %d, \"bp_ret_mismatch\": %d, \"bp_uu_mismatch\": %d, \"bp_cc_hat_mismatch\": %d, "
-         "\"bp_syndrom_soft_mismatch\": %d, \"err_bit_ref\": %d, \"err_bit_gpu\": %d}\n",
-         ncw, K, known_h ? 1 : 0, is5g ? 1 : 0, mm_km, mm_cand, mm_bp_ret, mm_bp_uu, mm_bp_cc, mm_bp_syn, err_ref,
-         err_gpu);
+         "\"bp_syndrom_soft_mismatch\": %d, \"kmeans_state_mismatch\": %d, \"err_bit_ref\": %d, "
+         "\"err_bit_gpu\": %d}\n",
+         ncw, K, known_h ? 1 : 0, is5g ? 1 : 0, mm_km, mm_cand, mm_bp_ret, mm_bp_uu, mm_bp_cc, mm_bp_syn, mm_kmstate,
+         err_ref, err_gpu);
   return 0;
 }

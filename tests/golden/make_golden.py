@@ -225,6 +225,42 @@ def make_soft(tmp):
               f"inf_metrics={int(np.isinf(arrs['metrics']).sum())}")
 
 
+# KMeans::clusters() / idx() fixtures: name -> (matrix, modem, snr, n)
+KMSTATE_CASES = {
+    "peg2304_qpsk_s2": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", 2.0, 16),
+    "peg2304_qpsk_sm1": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", -1.0, 8),
+    "peg2304_16qam_s5": ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", 5.01, 8),
+    "peg8064_64qam_s677": ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", 6.77, 4),
+}
+
+
+def make_kmstate(tmp):
+    """ref_harness mode kmstate -> golden/kmstate/<name>.npz (y, true_h, clusters, idx)."""
+    os.makedirs(os.path.join(HERE, "kmstate"), exist_ok=True)
+    for name, (mat, mod, snr, n) in KMSTATE_CASES.items():
+        cfg = os.path.join(tmp, name + ".toml")
+        write_toml(cfg, REF_CFG, mat, mod, False, False, 20, True)
+        out = os.path.join(tmp, name + ".bin")
+        subprocess.run([HARNESS, cfg, repr(snr), str(n), out, "kmstate"], check=True)
+        buf = open(out, "rb").read()
+        r = Reader(buf)
+        K, N, S, M, Kc = (struct.unpack_from("<i", buf, 4 * i)[0] for i in range(1, 6))
+        r.o = 4 * 10 + 8 + 16 * Kc
+        th, ys, cls, idxs = [], [], [], []
+        for _ in range(n):
+            th.append(r.f64(2))
+            ys.append(r.f64(2 * S).reshape(S, 2))
+            cls.append(r.f64(2 * Kc).reshape(Kc, 2))
+            idxs.append(np.frombuffer(buf, "<i4", S, r.o).copy())
+            r.o += 4 * S
+        assert r.o == len(buf)
+        hdr = dict(matrix=mat, modem=mod, snr=snr, n=n, S=S, Kc=Kc, iters=20)
+        np.savez_compressed(os.path.join(HERE, "kmstate", name + ".npz"),
+                            hdr_json=np.frombuffer(json.dumps(hdr).encode(), dtype=np.uint8), true_h=np.stack(th),
+                            y=np.stack(ys), clusters=np.stack(cls), idx=np.stack(idxs).astype(np.int32))
+        print(f"{name}: n={n} S={S} Kc={Kc} idx counts {np.bincount(np.concatenate(idxs), minlength=Kc)[:8]}")
+
+
 def make_rng(tmp, n=2000):
     """Reference RNG streams with SetSeed(-1) -> golden/host/rng.npz."""
     out = os.path.join(tmp, "rng.bin")
@@ -365,7 +401,8 @@ def make_bench_large(tmp):
 
 
 def main():
-    for flag, fn in (("--bench", make_bench), ("--sweep", make_sweep), ("--bench-large", make_bench_large)):
+    for flag, fn in (("--bench", make_bench), ("--sweep", make_sweep), ("--bench-large", make_bench_large),
+                     ("--kmstate", make_kmstate)):
         if flag in sys.argv:
             tmp = tempfile.mkdtemp()
             try:

@@ -4,7 +4,8 @@ compiled in the build container + integration/kmldpc_gpu_codecs.hpp + the
 product library).  Every codeword of the reference's seed-17 stream goes
 through lab::BinaryLDPCCodec::Decoder and GpuBinaryLDPCCodec::Decoder,
 KmCodec::Decoder and GpuKmCodec::Decoder, the reference KMeans and
-gpu_kmeans_h_hats: no mismatch is allowed in any output."""
+gpu_kmeans_h_hats / GpuKMeans (clusters, idx, DumpToMat): no mismatch is
+allowed in any output."""
 import json
 import os
 import subprocess
@@ -33,6 +34,12 @@ def test_reference_side_shims_match_reference_classes(data_dir, tmp_path, matrix
     print(res)
     assert res["codewords"] == n
     for k in ("kmcodec_uu_mismatch", "candidate_mismatch", "bp_ret_mismatch", "bp_uu_mismatch", "bp_cc_hat_mismatch",
-              "bp_syndrom_soft_mismatch"):
+              "bp_syndrom_soft_mismatch", "kmeans_state_mismatch"):
         assert res[k] == 0, k
     assert res["err_bit_ref"] == res["err_bit_gpu"] and res["err_bit_ref"] > 0
+    if not known:  # GpuKMeans::DumpToMat of the first codeword, read back
+        import scipy.io
+        m = scipy.io.loadmat(str(tmp_path / "kmeans0.mat"))
+        S, Kc = m["data"].shape[0], m["cluster"].shape[0]
+        assert m["idx"].dtype == "int32" and m["idx"].shape == (S, 1) and m["hHats"].shape == (4, 1)
+        assert m["constellations"].shape == (Kc, 1) and m["realH"].shape == (1, 1)

@@ -617,3 +617,54 @@ def test_soft_metric_histogram_matches_reference(data_dir):
     assert np.array_equal(out["chosen"], z["chosen"])
     assert np.array_equal(out["uu_hat"], uh)
     ctx.close()
+
+
+KMSTATE = sorted(f[:-4] for f in os.listdir(os.path.join(os.path.dirname(__file__), "golden", "kmstate")))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", KMSTATE)
+def test_kmeans_state_vs_reference(name, data_dir):
+    """kml_kmeans_state = KMeans::clusters() and idx() after Run, on the
+    reference's own frames and outputs (golden/kmstate, ref_harness), plus the
+    oracle on fresh frames of the same configuration."""
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "kmstate", name + ".npz"))
+    hdr = json.loads(bytes(z["hdr_json"]).decode())
+    ctx = ctx_for(data_dir, hdr["matrix"], hdr["modem"], False)
+    cl, idx = ctx.kmeans_state(z["y"], hdr["iters"])
+    assert np.array_equal(cl, z["clusters"])
+    assert np.array_equal(idx, z["idx"])
+    oc = oracle_for(data_dir, hdr["matrix"], False)
+    om = O.Modem(os.path.join(data_dir, hdr["modem"]))
+    _, _, _, y = O.gen_frames(oc, om, hdr["snr"], 3 * hdr["n"], state=5)
+    cl, idx = ctx.kmeans_state(y)
+    for b in range(y.shape[0]):
+        rc, ri = O.kmeans_state(y[b], om.points)
+        assert np.array_equal(cl[b], rc) and np.array_equal(idx[b], ri), b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("modem", ["2bits_QPSK.txt", "4bit_16QAM_Gray.txt", "6bits_64QAM_Gray.txt"])
+def test_kmeans_state_adversarial_ties(data_dir, modem):
+    """Final assignment with exact distance ties (symbols on midpoints between
+    clusters, at zero, on points): idx is the FIRST minimum (min_element)."""
+    matrix = "PEG8064regular0.5.txt" if "64QAM" in modem else "PEG2304regular0.5.txt"
+    ctx = ctx_for(data_dir, matrix, modem, False)
+    om = O.Modem(os.path.join(data_dir, modem))
+    pts = om.points.reshape(-1, 2)
+    rng = np.random.default_rng(23)
+    S, B = ctx.S, 12
+    y = np.zeros((B, S, 2))
+    for b in range(B):
+        hc = complex(1.0, 0.0) if b % 2 == 0 else complex(*rng.normal(size=2))
+        p1 = pts[rng.integers(0, len(pts), S)] @ [1, 1j]
+        p2 = pts[rng.integers(0, len(pts), S)] @ [1, 1j]
+        kinds = rng.integers(0, 4, S)
+        zz = np.where(kinds == 0, p1 * hc, np.where(kinds == 1, (p1 + p2) / 2 * hc,
+                      np.where(kinds == 2, 0.0, p1 * hc + 1e-3 * (rng.normal(size=S) + 1j * rng.normal(size=S)))))
+        y[b, :, 0], y[b, :, 1] = zz.real, zz.imag
+    cl, idx = ctx.kmeans_state(y)
+    for b in range(B):
+        rc, ri = O.kmeans_state(y[b], om.points)
+        assert np.array_equal(cl[b], rc, equal_nan=True), b
+        assert np.array_equal(idx[b], ri), b

@@ -3,6 +3,7 @@ every symbol include/kmldpc_amd.h declares, the host planner (config parsing,
 H-matrix parsing, GF(2) elimination, graph order, encoder, constellation) is
 bit-identical to the oracle, and the exact-math restatements used by the
 device code equal glibc / libgcc on the host."""
+import json
 import os
 import subprocess
 import sys
@@ -263,3 +264,35 @@ def test_first_backward_normalisation_is_identity():
     one_minus = 1.0 - c0
     assert np.all(c0 + one_minus == 1.0)
     assert np.all(c0 / (c0 + one_minus) == c0) and np.all(one_minus / (c0 + one_minus) == one_minus)
+
+
+def test_kmeans_dump_mat_level5(tmp_path, data_dir):
+    """KMeans::DumpToMat (src/kmeans.cc:99-109) through kml_kmeans_dump_mat:
+    a MAT-file level 5 that scipy reads back with the reference's variable
+    names, classes (complex double, int32) and n x 1 shapes (lib/lab/src/mat.cc
+    WriteVector / WriteComplex), values bit-identical.  The data are the
+    reference's own k-means state (golden/kmstate)."""
+    import scipy.io
+
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "kmstate", "peg2304_16qam_s5.npz"))
+    hdr = json.loads(bytes(z["hdr_json"]).decode())
+    om = O.Modem(os.path.join(data_dir, hdr["modem"]))
+    y, cl, idx = z["y"][1], z["clusters"][1], z["idx"][1]
+    cons = om.points.reshape(-1, 2)
+    hh = cl[0, 0] + 1j * cl[0, 1]
+    c0 = cons[0, 0] + 1j * cons[0, 1]
+    append = np.array([hh / c0 * 1j ** j for j in range(4)] + [z["true_h"][1, 0] + 1j * z["true_h"][1, 1]])
+    path = str(tmp_path / "km.mat")
+    K.dump_kmeans_mat(path, y, cl, idx, cons, append)
+    m = scipy.io.loadmat(path)
+    assert m["__version__"] == "1.0"
+    c = lambda a: a[:, 0] + 1j * a[:, 1]
+    for name, want, dt in [("data", c(y), np.complex128), ("cluster", c(cl), np.complex128),
+                           ("idx", idx, np.int32), ("constellations", c(cons), np.complex128),
+                           ("hHats", append[:4], np.complex128), ("realH", append[4:], np.complex128)]:
+        got = m[name]
+        assert got.dtype == dt, name
+        assert got.shape == (len(want), 1), name
+        assert np.array_equal(got[:, 0], want), name
+    with pytest.raises(K.KmlError):
+        K.dump_kmeans_mat(str(tmp_path / "no" / "such" / "dir.mat"), y, cl, idx, cons, append)

@@ -239,3 +239,20 @@ def test_oracle_reproduces_cfg5_sweep_fixture(data_dir):
         assert int(e.sum()) == z["counters"][p][0] and int((e > 0).sum()) == z["counters"][p][1]
         got = _oracle_errs(data_dir, "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, False, 20, float(snr), 6)
         assert np.array_equal(got, e[:6]), snr
+
+
+KMSTATE = sorted(f[:-4] for f in os.listdir(os.path.join(os.path.dirname(__file__), "golden", "kmstate")))
+
+
+@pytest.mark.parametrize("name", KMSTATE)
+def test_oracle_kmeans_state_matches_reference(name, data_dir):
+    """KMeans::clusters() and idx() after Run, from the reference itself
+    (golden/kmstate, ref_harness mode kmstate): the oracle restatement
+    (orc_kmeans_state) reproduces them bit for bit."""
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "kmstate", name + ".npz"))
+    hdr = json.loads(bytes(z["hdr_json"]).decode())
+    om = O.Modem(os.path.join(data_dir, hdr["modem"]))
+    for b in range(hdr["n"]):
+        cl, idx = O.kmeans_state(z["y"][b], om.points, hdr["iters"])
+        assert np.array_equal(cl, z["clusters"][b]), b
+        assert np.array_equal(idx, z["idx"][b]), b
