@@ -801,12 +801,22 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
 // symmetric argument holds for c2v, and across codewords the early-stop flags
 // of iteration g (posted after the member's loads of iteration g) gate the
 // next codeword's first writes.
-// Early stop: after its CN phase every member posts (g + 1, failing rows?) to
-// its flag word of parity g & 1, and wave 0 polls the members' flags (one per
-// lane) after its c2v receive.  A flag word is rewritten (iteration g + 2)
-// only after every member passed iteration g + 1's closing barrier, which
-// follows its poll of the iteration-g flags.  (Per-wave flags posted without
-// the CN-closing barrier measured slower: 9.30 vs 8.71 ms per 4096 cw.)
+// Early stop, checked one phase late: after its CN phase of iteration g the
+// member's LAST wave to finish (an LDS arrival count, no workgroup barrier)
+// posts (g + 1, failing rows?) to its flag word of parity g & 1, and wave 0
+// polls the members' flags (one per lane) after the NEXT VN phase, beside
+// the v2c receive — by then the flags have long arrived.  A codeword whose
+// checks all hold after iteration g therefore also runs VN g + 1 (its
+// decisions go to the other half of a double-buffered decision array; the
+// outputs take iteration g's half) and then stops, before CN g + 1.  VN
+// g + 1's v2c messages were received; the c2v entries still hold iteration
+// g - 1's tag parity, which the next codeword's first CN (iteration g + 2)
+// would match, so the stopping members overwrite their c2v entries with tag
+// g + 1 (a flush nobody reads) before the codeword's closing barrier.
+// A flag word is rewritten (iteration g + 2) only after the poster received
+// the v2c of iteration g + 2, which its partners send after their iteration
+// g + 1 flag polls.  Measured against the CN-closing-barrier form (flags
+// checked before the next VN): see DESIGN.md.
 constexpr unsigned kTagHi = 0x80000000u;  // bit 63 of a message word (hi dword bit 31)
 constexpr unsigned kHdHi = 0x40000000u;   // bit 62: hard decision (v2c first word)
 
@@ -888,26 +898,34 @@ __device__ __forceinline__ bool poll_entries(const int (&ent)[R], __amdgpu_buffe
 template <int kG, int T, int RV, int RC, int RX, bool SYN>
 __device__ __forceinline__ bool part_iterations_tagged(
     const BpLaunch &a, int M, int cw, GroupSync *gs, unsigned &g, int *sfail, int *sdead, int member,
-    unsigned *abort, unsigned char *smem, uint8_t *dec, __amdgpu_buffer_rsrc_t tb, unsigned tb_c2v,
+    unsigned *abort, unsigned char *smem, uint8_t *dec, int NG, __amdgpu_buffer_rsrc_t tb, unsigned tb_c2v,
     const int (&vaddr)[RV][3],
-    const int (&vpos)[RV], const bool (&vact)[RV], const double (&pv)[RV], const int (&crow)[RC],
+    const bool (&vact)[RV], const double (&pv)[RV], const int (&crow)[RC],
     const int (&cbase)[RC], const int (&crx)[RC], const bool (&cact)[RC], const int (&xr)[RX], const int (&xc)[RX],
-    int odd, int &iter_out, bool &conv_out, int &pcnt_out) {
-  constexpr int DV = 3, DC = 6, H = 3;
+    int odd, int &iter_out, bool &conv_out, int &pcnt_out, int &decbuf_out) {
+  constexpr int DV = 3, DC = 6, H = 3, NW = T / 64;
   const int tid = threadIdx.x;
-  int iter = 0, pcnt = 0;
+  __shared__ int sarrive;  // waves done with the CN phase of this iteration
+  __shared__ int sany;     // some member had failing rows after the previous CN phase
+  if (tid == 0) sarrive = 0;
+  int iter = 0, pcnt_prev = 0;
+  double syn_prev[RC];
+#pragma unroll
+  for (int r = 0; r < RC; ++r) syn_prev[r] = 0.0;
   bool conv = false;
 #ifdef KML_STAMPS
   unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
 #endif
-  for (; iter < a.iter_count; ++iter, ++g) {
+  for (;; ++iter, ++g) {
     const unsigned tag = g & 1u;
+    const bool run = iter < a.iter_count;  // else only the last CN phase's early-stop check remains
+    uint8_t *decb = dec + (iter & 1) * NG;
     KML_STAMP(0);
     // ------------------------------------------------------------ VN phase
     // (c2v of cut edges sit in the mirror slots, received at the end of the
     // previous iteration; iteration 0 reads InitMsg's 0.5)
-    __builtin_amdgcn_s_setprio(3);
-    {
+    if (run) {
+      __builtin_amdgcn_s_setprio(3);
       double c0s[RV][DV];
 #pragma unroll
       for (int r = 0; r < RV; ++r)
@@ -935,7 +953,7 @@ __device__ __forceinline__ bool part_iterations_tagged(
           } else {
             const int hd = hard_decision<true>(n0, n1);
             hdb[r] = hd ? kHdHi : 0u;
-            if (vact[r]) dec[vpos[r]] = (unsigned char)hd;
+            if (vact[r]) decb[r * T + tid] = (unsigned char)hd;
           }
         }
       double b0[RV], b1[RV];
@@ -978,18 +996,63 @@ __device__ __forceinline__ bool part_iterations_tagged(
       }
     }
     KML_STAMP(2);
-    // ------------------------------------------- receive v2c of the cut edges
-    if (!poll_entries<RX, 2>(xr, tb, 0u, smem, tag, abort)) *sdead = 1;
+    // ------------------- receive v2c of the cut edges; the previous CN's flags
+    if (run)
+      if (!poll_entries<RX, 2>(xr, tb, 0u, smem, tag, abort)) *sdead = 1;
     KML_STAMP(4);
+    if (iter > 0 && tid < 64) {  // wave 0: lane m polls member m's flag of iteration g - 1
+      unsigned long long v = (unsigned long long)g << 1;
+      if (tid < kG) {
+        for (long long spin = 0;; ++spin) {
+          v = ld_rlx64(&gs->mflag[(g - 1) & 1][tid]);
+          if ((v >> 1) == (unsigned long long)g) break;
+          if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
+            __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *sdead = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      const bool any = __ballot((v & 1) != 0) != 0;
+      if (tid == 0) sany = any ? 1 : 0;
+    }
     __syncthreads();
     KML_STAMP(5);
     if (*sdead) return false;
+    if (iter > 0 && !sany) {  // every row satisfied after iteration iter - 1: stop before its CN phase
+      conv = true;
+      --iter;
+      if (iter + 1 < a.iter_count) {  // VN iter + 1 ran: flush the c2v entries (see above)
+        const double dummy = or_hi(0.5, tag ? kTagHi : 0u);
+#pragma unroll
+        for (int r = 0; r < RC; ++r)
+          if (cact[r]) {
+            const int mask = crx[r] & 0xFF;
+#pragma unroll
+            for (int k = 0; k < H; ++k) {
+              const int e = odd ? H + k : k;
+              if ((mask >> e) & 1) mb_st64(tb, tb_c2v + (unsigned)((crx[r] >> 8) + __popc(mask & ((1 << e) - 1))) * 8,
+                                           dummy);
+            }
+          }
+        ++g;
+      }
+      break;
+    }
+    if constexpr (SYN) {  // the previous CN phase counted: its syndromes stand (alpha past the last edge, :274)
+      if (iter > 0) {
+#pragma unroll
+        for (int r = 0; r < RC; ++r)
+          if (cact[r] && !odd) a.syn[(long long)cw * M + crow[r]] = syn_prev[r];
+      }
+    }
+    if (!run) break;  // max iterations without convergence
 
     // ------------------------------------------ CN phase (+ the parity check)
     // bp_regular.hip's step order: every load of a step before its stores.
     // A message's first word carries the column's hard decision in bit 62
     // (the receive strips the mailbox tags).
-    double syn0[RC];
     int par[RC];
     {
       double x0[RC][H], x1[RC][H];
@@ -1052,7 +1115,7 @@ __device__ __forceinline__ bool part_iterations_tagged(
         }
       }
 #pragma unroll
-      for (int r = 0; r < RC; ++r) syn0[r] = s0[r];
+      for (int r = 0; r < RC; ++r) syn_prev[r] = s0[r];
     }
     // the row's parity: the even lane XORed edges 0..2, the odd lane 5..3
     int fail = 0, nfail = 0;
@@ -1062,55 +1125,31 @@ __device__ __forceinline__ bool part_iterations_tagged(
       fail |= cact[r] ? full : 0;
       nfail += (cact[r] && !odd) ? full : 0;
     }
-    pcnt = nfail;  // unsatisfied checks of this iteration's hard decisions (final if the loop ends here)
-    if (__ballot(fail) != 0 && (tid & 63) == 0) atomicOr(sfail, 1);
+    pcnt_prev = nfail;  // unsatisfied checks of this iteration's hard decisions (final if the loop ends after it)
+    const bool wfail = __ballot(fail) != 0;
     KML_STAMP(6);
-    __syncthreads();
-    KML_STAMP(7);
-    // ------------- post this member's flag; receive c2v; read the others' flags
-    __shared__ int sany;
-    if (tid == 0) {
-      const unsigned long long mine = ((unsigned long long)(g + 1) << 1) | (unsigned long long)(*sfail != 0);
-      *sfail = 0;
-      __hip_atomic_store(&gs->mflag[g & 1][member], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((tid & 63) == 0) {  // the member's last wave to get here posts its flag
+      if (wfail) atomicOr(sfail, 1);
+      if (atomicAdd(&sarrive, 1) == NW - 1) {
+        const int f = atomicExch(sfail, 0);
+        sarrive = 0;
+        __hip_atomic_store(&gs->mflag[g & 1][member], ((unsigned long long)(g + 1) << 1) | (unsigned long long)(f != 0),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
+    KML_STAMP(7);
+    // --------------------------------------- receive c2v of the cut edges
     if (iter + 1 < a.iter_count)
       if (!poll_entries<RX, 1>(xc, tb, tb_c2v, smem, tag, abort)) *sdead = 1;
-    if (tid < 64) {  // wave 0: lane m polls member m's flag
-      unsigned long long v = (unsigned long long)(g + 1) << 1;
-      if (tid < kG) {
-        for (long long spin = 0;; ++spin) {
-          v = ld_rlx64(&gs->mflag[g & 1][tid]);
-          if ((v >> 1) == (unsigned long long)(g + 1)) break;
-          if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
-            __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            *sdead = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      const bool any = __ballot((v & 1) != 0) != 0;
-      if (tid == 0) sany = any ? 1 : 0;
-    }
     __syncthreads();
     KML_STAMP(8);
     if (*sdead) return false;
-    if (!sany) {  // every row satisfied: stop before this CN phase
-      conv = true;
-      pcnt = 0;
-      ++g;
-      break;
-    }
-    if constexpr (SYN) {
-#pragma unroll
-      for (int r = 0; r < RC; ++r)
-        if (cact[r] && !odd) a.syn[(long long)cw * M + crow[r]] = syn0[r];  // alpha past the last edge (:274)
-    }
   }
   iter_out = iter;
   conv_out = conv;
-  pcnt_out = pcnt;
+  pcnt_out = conv ? 0 : pcnt_prev;
+  decbuf_out = iter & 1;  // the decisions of the last counted VN phase (iteration iter, or iter - 1 at max)
+  if (!conv) decbuf_out = (iter - 1) & 1;
   return true;
 }
 
@@ -1224,7 +1263,7 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     const bool fast = (fast_allowed & 1) && !ld_rlx(&gs->nofast);
     constexpr bool tagged = TAGGED;
 
-    int iter = 0, pcnt = 0;
+    int iter = 0, pcnt = 0, decbuf = 0;
     bool conv = false;
     bool alive;
     if constexpr (TAGGED) {
@@ -1233,8 +1272,8 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
         continue;
       }
       alive = part_iterations_tagged<kG, T, RV, RC, RX, SYN>(a, c.M, cw, gs, g, &sfail, &sdead, member, abort, smem, dec,
-                                                          tb, tb_c2v, vaddr, vpos, vact, pv, crow, cbase, crx,
-                                                          cact, xr, xc, odd, iter, conv, pcnt);
+                                                          NG, tb, tb_c2v, vaddr, vact, pv, crow, cbase, crx, cact,
+                                                          xr, xc, odd, iter, conv, pcnt, decbuf);
     } else if (fast) {
       alive = part_iterations<kG, RV, RC, RX, SYN, true>(a, c.M, c.N, NG, cw, gs, bst, nb, &sfail, same_xcd, abort, smem, dec,
                                                          mb_v2c, mb_c2v, gc, c, vaddr, vpos, vact, pv, crow, cbase,
@@ -1249,10 +1288,11 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     // ---- outputs
     if (a.iter_count > 0) {
       if constexpr (tagged) {
-        // a member holds the decisions of its own columns: it writes theirs
+        // a member holds the decisions of its own columns (double-buffered by
+        // iteration, dec[2][NG]): it writes theirs
         for (int p = member * NG + tid; p < (member + 1) * NG; p += T) {
           const int col = c.pt_vn[p];
-          const int hd = dec[p];
+          const int hd = dec[decbuf * NG + (p - member * NG)];
           if (a.cc_hat) a.cc_hat[(long long)cw * c.N + col] = (uint8_t)hd;
           const int i = col - c.info_off;
           if (i >= 0 && i < c.K) {

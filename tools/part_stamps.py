@@ -20,9 +20,9 @@ os.environ.setdefault("KML_LIB", os.path.join(REPO, "kmldpc_amd", "libkmldpc_amd
 import kmldpc_amd as K  # noqa: E402
 
 # the tagged exchange (default) stamps: 0 loop top, 2 VN compute, 4 v2c poll,
-# 5 sync, 6 parity + CN compute, 7 sync, 8 flag post + c2v poll + flags poll + sync
-TAGGED_NAMES = ["iteration boundary", "-", "VN compute (wave 0)", "-", "poll v2c (wave 0)", "sync after v2c receive",
-                "CN compute + parity (wave 0)", "CN drain (sync)", "flag + c2v poll + flags + sync", "-"]
+# 5 previous flags poll + sync, 6 parity + CN compute, 7 flag post (last wave), 8 c2v poll + sync
+TAGGED_NAMES = ["iteration boundary", "-", "VN compute (wave 0)", "-", "poll v2c (wave 0)",
+                "prev. flags poll + sync", "CN compute + parity (wave 0)", "flag post", "c2v poll + sync", "-"]
 NAMES = ["iteration boundary", "receive c2v (+sync)", "VN compute (wave 0)", "VN drain (sync)",
          "send v2c + group barrier", "receive v2c + decisions (+sync)", "parity + CN compute (wave 0)",
          "CN drain (sync)", "send c2v + group barrier (+flags)", "-"]
