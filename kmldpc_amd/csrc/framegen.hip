@@ -13,6 +13,8 @@
 // independent of the batch size and of the number of GPUs (weak-scaling
 // invariant), and BER/FER are checked against the reference within Monte-Carlo
 // confidence.  Bit-exact parity runs feed the reference's own frames instead.
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace kml {
@@ -112,6 +114,60 @@ __global__ __launch_bounds__(256) void encode_kernel(DevCode c, int B, int Cw, c
   if ((threadIdx.x & 63) == 0) cc[(long long)cw * Cw + (i >> 6)] = mask;
 }
 
+// The parity part of the same encoder for codes whose parity and info runs
+// start on 64-bit word boundaries of cc (PEG2304, PEG8064, 5G BG2 K960): a
+// workgroup takes 64 parity rows x kEncCw codewords.  The rows' generator
+// words are staged in LDS transposed (word w of row r at [w][r]: lane r reads
+// consecutive addresses), the codewords' info words likewise ([cw][w], one
+// broadcast per word); lane r of a wave forms parity bit r of one codeword
+// per pass (AND / XOR over Kw words, popcount parity) and the wave packs the
+// 64 bits with a ballot.  Each generator word is read from HBM once per
+// kEncCw codewords instead of once per codeword, and every global access is
+// coalesced (the one-lane-per-bit encode_kernel reads 64 rows per load).
+constexpr int kEncCw = 64;
+__global__ __launch_bounds__(256) void encode_parity_kernel(DevCode c, int B, int Cw, int par_word,
+                                                            const uint64_t *__restrict__ uu,
+                                                            uint64_t *__restrict__ cc) {
+  extern __shared__ uint64_t es[];
+  const int Kw = c.Kw;
+  uint64_t *gt = es;            // [Kw][64]
+  uint64_t *us = es + Kw * 64;  // [kEncCw][Kw]
+  const int r0 = blockIdx.x * 64, c0 = blockIdx.y * kEncCw;
+  const int ncw = min(kEncCw, B - c0);
+  for (int idx = threadIdx.x; idx < 64 * Kw; idx += blockDim.x) {
+    const int r = idx / Kw, w = idx - r * Kw;
+    gt[w * 64 + r] = r0 + r < c.chk ? c.enc_info[(long long)(r0 + r) * Kw + w] : 0ull;
+  }
+  for (int idx = threadIdx.x; idx < ncw * Kw; idx += blockDim.x) us[idx] = uu[(long long)c0 * Kw + idx];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int k = wave; k < ncw; k += blockDim.x / 64) {
+    const uint64_t *u = us + k * Kw;
+    uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    int w = 0;
+    for (; w + 4 <= Kw; w += 4) {
+      a0 ^= gt[(w + 0) * 64 + lane] & u[w + 0];
+      a1 ^= gt[(w + 1) * 64 + lane] & u[w + 1];
+      a2 ^= gt[(w + 2) * 64 + lane] & u[w + 2];
+      a3 ^= gt[(w + 3) * 64 + lane] & u[w + 3];
+    }
+    for (; w < Kw; ++w) a0 ^= gt[w * 64 + lane] & u[w];
+    const int bit = __popcll(a0 ^ a1 ^ a2 ^ a3) & 1;
+    const uint64_t mask = __ballot(bit);
+    if (lane == 0) cc[(long long)(c0 + k) * Cw + par_word + blockIdx.x] = mask;
+  }
+}
+
+// the info part of cc for the same codes: a word-aligned copy of uu's words
+// [info_word0, info_word0 + n) to cc words [cc_word0, ...)
+__global__ void encode_info_kernel(int B, int Kw, int Cw, int info_word0, int cc_word0, int n,
+                                   const uint64_t *__restrict__ uu, uint64_t *__restrict__ cc) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long long)B * n) return;
+  const int cw = (int)(gid / n), w = (int)(gid - (long long)cw * n);
+  cc[(long long)cw * Cw + cc_word0 + w] = uu[(long long)cw * Kw + info_word0 + w];
+}
+
 // one thread per symbol: Mapping + y = x*h + n*(sigma/sqrt2)
 __global__ __launch_bounds__(256) void channel_kernel(int bits, const double *__restrict__ cons, int S, int Cw, int B,
                                                       unsigned long long seed, unsigned long long first_cw,
@@ -148,7 +204,22 @@ hipError_t launch_framegen(const DevCode &c, int bits, const double *cons, const
     hipLaunchKernelGGL(source_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c.K, c.Kw, f.B, f.seed,
                        f.first_cw, c.active, f.uu_bits);
   }
-  {
+  // word-aligned layout: PEG cc = [parity(chk) | info(K)]; 5G cc = info bits
+  // [punct, K) then the parity bits (the first 2Z info bits are punctured)
+  const int info_cc0 = c.is5g ? 0 : c.chk, par_cc0 = c.is5g ? c.K - c.punct : 0;
+  const int info_u0 = c.is5g ? c.punct : 0, ninfo = c.is5g ? c.K - c.punct : c.K;
+  const int npar = c.cc_len - ninfo;  // transmitted parity bits (rows 0..npar-1 of the generator)
+  const size_t elds = sizeof(uint64_t) * ((size_t)c.Kw * 64 + (size_t)kEncCw * c.Kw);
+  const bool aligned = c.active && npar > 0 && npar <= c.chk && npar % 64 == 0 && info_cc0 % 64 == 0 &&
+                       par_cc0 % 64 == 0 && info_u0 % 64 == 0 && ninfo % 64 == 0 &&
+                       (c.is5g ? par_cc0 + npar == c.cc_len : info_cc0 == npar) && elds <= 64 * 1024;
+  if (aligned && !getenv("KML_ENCODE_LANE")) {
+    hipLaunchKernelGGL(encode_parity_kernel, dim3((unsigned)(npar / 64), (unsigned)((f.B + kEncCw - 1) / kEncCw)),
+                       dim3(256), elds, s, c, f.B, Cw, par_cc0 / 64, f.uu_bits, f.cc_bits);
+    const long long n = (long long)f.B * (ninfo / 64);
+    hipLaunchKernelGGL(encode_info_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, f.B, c.Kw, Cw,
+                       info_u0 / 64, info_cc0 / 64, ninfo / 64, f.uu_bits, f.cc_bits);
+  } else {
     const long long n = (long long)f.B * Cw * 64;
     hipLaunchKernelGGL(encode_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c, f.B, Cw, f.uu_bits,
                        f.cc_bits);

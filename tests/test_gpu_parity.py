@@ -668,3 +668,28 @@ def test_kmeans_state_adversarial_ties(data_dir, modem):
         rc, ri = O.kmeans_state(y[b], om.points)
         assert np.array_equal(cl[b], rc, equal_nan=True), b
         assert np.array_equal(idx[b], ri), b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("matrix,modem,is5g", [
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False),
+    ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True),
+    ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False),
+])
+def test_gpu_encoder_equals_host_encoder(data_dir, matrix, modem, is5g):
+    """The GPU frame generator's encoder (framegen.hip) equals the host encoder
+    (BinaryLDPCCodec::Encoder restated, kml_encode) bit for bit: at 60 dB the
+    nearest constellation point of y / h gives back the transmitted label
+    bits (MSB first, modem.cc:12-21), which must be encode(uu)."""
+    ctx = ctx_for(data_dir, matrix, modem, is5g)
+    B = 200
+    ctx.sim_generate(60.0, B, seed=9, first_cw=77)
+    uu, y, h = ctx.sim_frames(B)
+    pts = ctx.constellation().reshape(-1, 2)
+    pc = pts[:, 0] + 1j * pts[:, 1]
+    x = (y[:, :, 0] + 1j * y[:, :, 1]) / (h[:, 0] + 1j * h[:, 1])[:, None]
+    lab = np.abs(x[:, :, None] - pc[None, None, :]).argmin(axis=2)
+    bits = ctx.bits
+    cc_gpu = ((lab[:, :, None] >> np.arange(bits - 1, -1, -1)) & 1).reshape(B, -1).astype(np.uint8)
+    cc_host = ctx.encode(uu)
+    assert np.array_equal(cc_gpu, cc_host)
