@@ -285,7 +285,7 @@ __global__ void km_final_kernel(const double *__restrict__ cons, const double *_
 //     __divdc3's own branch with the constant parts hoisted (exact: same
 //     operations on the same values).
 // Measured (MI355X, 32768 PEG2304/QPSK codewords at Es/N0 2 dB, 19.9
-// iterations each): 4.28 ms -> 3.44 ms; tools/km_stamps.py gives the phases.
+// iterations each): 4.28 ms -> 3.31 ms; tools/km_stamps.py gives the phases.
 constexpr int kFusedT = 128;  // two waves per codeword (the two sum chains), up to 7 codewords per CU (LDS)
 constexpr int kFusedMaxW = 64;  // 64-symbol words: S <= 4096
 
@@ -412,15 +412,26 @@ __device__ __forceinline__ double ordered_sum(double acc, const double *yv, cons
 // leaves the binade.  Each lane takes kScanPer consecutive elements, rounds
 // them to the grid (v_rndne), sums them locally, and a DPP exclusive scan of
 // the lane totals gives every prefix A + P.  All elements before the first one
-// that is a tie, large (|X| >= 2^51: keeps every partial sum of valid elements
-// below 2^53, hence exact), or whose prefix leaves [2^52 + 1, 2^53 - 1] (then
-// the exact sum lies inside the binade, where RN is the grid rounding) are
-// exact; that element is added with a real fp64 add and the scan resumes after
-// it.  A zero or non-finite sum, and runs after an early exit, are added one
-// by one.  On MI355X a dependent f64 add chain costs ~40 cycles per element
-// here (LDS index + value loads, other waves on the SIMD); a step of 256
-// elements costs about 50 dependent instructions.
-constexpr int kScanPer = 4;  // 8 per lane measured slower (3.89 vs 3.44 ms per 32768 QPSK cw)
+// that is large (|X| >= 2^51: keeps every partial sum of valid elements below
+// 2^53, hence exact) or whose prefix leaves [2^52 + 1, 2^53 - 1] (then the
+// exact sum lies inside the binade, where RN is the grid rounding) are exact;
+// that element is added with a real fp64 add and the scan resumes after it.
+// Ties do not stop the scan: they count floor(X), and afterwards, in element
+// order, each tie whose corrected prefix is odd rounds up (ties to even),
+// adding 1 to every later prefix (kScanMargin keeps the range test valid
+// under those corrections).  A zero or non-finite sum, and runs after an
+// early exit, are added one by one.  On MI355X a dependent f64 add chain
+// costs ~40 cycles per element here (LDS index + value loads, other waves on
+// the SIMD); a step costs about 50 dependent instructions.
+// elements per lane per step: 5 covers a QPSK cluster-0 list (~286) in one
+// step; measured per 32768 PEG2304/QPSK codewords: 4 -> 3.42 ms, 5 -> 3.31 ms,
+// 8 -> 3.89 ms (longer in-lane chains and registers)
+#ifndef KML_KM_SCAN_PER
+#define KML_KM_SCAN_PER 5
+#endif
+constexpr int kScanPer = KML_KM_SCAN_PER;
+constexpr double kScanMargin = 64.0;      // grid steps kept from the binade ends: room for the tie corrections
+constexpr int kScanMaxTies = 32;          // ties resolved in one step (each moves later prefixes by <= 1)
 template <int CTRL, int ROWS>
 __device__ __forceinline__ double dpp_add_step(double v) {
   const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWS, 0xF, false);
@@ -470,50 +481,94 @@ __device__ double ordered_sum_wave(double acc, const double *yv, const unsigned 
     const int e = __builtin_amdgcn_frexp_exp(acc);  // |acc| in [2^(e-1), 2^e)
     const double sg = acc < 0.0 ? -1.0 : 1.0;
     const double A = __builtin_amdgcn_ldexp(fabs(acc), 53 - e);
-    double L[kScanPer];
-    unsigned badm = 0;
+    double T[kScanPer];
+    unsigned bigm = 0, tiem = 0;
     double run = 0.0;
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
       const double X = __builtin_amdgcn_ldexp(sg * x[k], 53 - e);
-      const bool bad = !(fabs(X) < 0x1p51) || (X - floor(X)) == 0.5;
-      badm |= (bad ? 1u : 0u) << k;
-      run = run + (bad ? 0.0 : rint(X));
-      L[k] = run;
+      const double fl = floor(X);
+      const bool big = !(fabs(X) < 0x1p51);
+      const bool tie = !big && (X - fl) == 0.5;
+      bigm |= (big ? 1u : 0u) << k;
+      tiem |= (tie ? 1u : 0u) << k;
+      // a tie counts its lower neighbour; the parity pass below adds 1 where it rounds up
+      run = run + (big ? 0.0 : (tie ? fl : rint(X)));
+      T[k] = run;
     }
     const double E = wave_exclusive_scan(run);
     const int kl = min(max(c - kScanPer * lane, 0), kScanPer);  // this lane's elements
-    unsigned outm = 0;
+    const int pos0 = kScanPer * lane;                           // their positions in the step
+    unsigned hardm = 0;
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
-      const double T = A + (E + L[k]);
-      const bool out = k < kl && (((badm >> k) & 1u) || !(T >= 0x1p52 + 1.0 && T <= 0x1p53 - 1.0));
-      outm |= (out ? 1u : 0u) << k;
+      T[k] = A + (E + T[k]);
+      const bool hard = k < kl && (((bigm >> k) & 1u) || !(T[k] >= 0x1p52 + kScanMargin && T[k] <= 0x1p53 - kScanMargin));
+      hardm |= (hard ? 1u : 0u) << k;
     }
-    const uint64_t ob = __ballot(outm != 0);
-    if (ob == 0) {
+    int fh = c;  // the first element that must be added for real
+    {
+      const uint64_t hb = __ballot(hardm != 0);
+      if (hb) {
+        const int lf = __builtin_ctzll(hb);
+        fh = kScanPer * lf + __builtin_amdgcn_readlane(__builtin_ctz(hardm | (1u << kScanPer)), lf);
+      }
+    }
+    // ties before fh, in order: round half to even on the corrected prefix
+    {
+      unsigned tm = 0;
+#pragma unroll
+      for (int k = 0; k < kScanPer; ++k)
+        if (pos0 + k < fh) tm |= tiem & (1u << k);
+      int nt = 0;
+      for (uint64_t tb = __ballot(tm != 0); tb; tb = __ballot(tm != 0)) {  // wave-uniform
+        const int lt = __builtin_ctzll(tb);
+        const int kt = __builtin_ctz((unsigned)__builtin_amdgcn_readlane((int)tm, lt));
+        const int q = kScanPer * lt + kt;
+        if (nt == kScanMaxTies) {  // too many ties for the margin: this one is added for real
+          fh = q;
+          break;
+        }
+        ++nt;
+        double ts = T[0];
+#pragma unroll
+        for (int k = 1; k < kScanPer; ++k)
+          if (kt == k) ts = T[k];
+        const double Tq = lane_d(ts, lt);
+        if ((long long)Tq & 1) {  // odd: the tie rounds up, and so does every later prefix
+#pragma unroll
+          for (int k = 0; k < kScanPer; ++k)
+            if (pos0 + k >= q) T[k] += 1.0;
+        }
+        if (lane == lt) tm &= ~(1u << kt);
+      }
+    }
+    if (fh == c) {
       const int kk = (c - 1) % kScanPer;
-      double Tl = A + (E + L[0]);
+      double Tl = T[0];
 #pragma unroll
       for (int k = 1; k < kScanPer; ++k)
-        if (kk == k) Tl = A + (E + L[k]);
+        if (kk == k) Tl = T[k];
       acc = sg * __builtin_amdgcn_ldexp(lane_d(Tl, (c - 1) / kScanPer), e - 53);
       i += c;
     } else {
-      const int lf = __builtin_ctzll(ob);
-      const int fk = __builtin_ctz(outm | (1u << kScanPer));  // meaningful in lane lf
-      double Tpre = A + E, xf = x[0];
+      const int lf = fh / kScanPer, fk = fh % kScanPer;
+      double Tpre = T[0], xf = x[0];
 #pragma unroll
-      for (int k = 1; k < kScanPer; ++k)
-        if (fk == k) {
-          Tpre = A + (E + L[k - 1]);
-          xf = x[k];
-        }
-      acc = sg * __builtin_amdgcn_ldexp(lane_d(Tpre, lf), e - 53);
-      acc = acc + lane_d(xf, lf);  // the exiting / tie / large element, rounded for real
-      const int f = kScanPer * lf + __builtin_amdgcn_readlane(fk, lf);
-      i += f + 1;
-      if (f < 16) seq = 32;  // exits close together: a short one-by-one run
+      for (int k = 1; k < kScanPer; ++k) {
+        if (fk == k) xf = x[k];
+        if (fk - 1 == k) Tpre = T[k];
+      }
+      // the prefix before fh: the previous element's (in this lane or the lane below), or A
+      double Tp = fk > 0 ? lane_d(Tpre, lf) : A;
+      if (fk == 0 && lf > 0) {
+        double Tlast = T[kScanPer - 1];
+        Tp = lane_d(Tlast, lf - 1);
+      }
+      acc = sg * __builtin_amdgcn_ldexp(Tp, e - 53);
+      acc = acc + lane_d(xf, lf);  // the exiting / large element, rounded for real
+      i += fh + 1;
+      if (fh < 16) seq = 32;  // exits close together: a short one-by-one run
     }
   }
   return acc;

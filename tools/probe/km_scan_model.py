@@ -3,10 +3,11 @@ replaces the sequential cluster-0 sum): the same steps in Python doubles,
 checked against the plain left-to-right sum on random, sign-changing,
 tie-heavy and extreme inputs.  Run: python tools/probe/km_scan_model.py"""
 import math
+import os
 import random
 import sys
 
-P = 4   # elements per lane per step
+P = int(os.environ.get("KML_SCAN_PER", "4"))  # elements per lane per step
 W = 64  # lanes
 
 
@@ -51,42 +52,60 @@ def wave_sum(acc, xs, stats):
         sg = -1.0 if acc < 0.0 else 1.0
         A = ldexp(abs(acc), 53 - e)
         L = [[0.0] * P for _ in range(W)]
-        badm = [0] * W
+        bigm = [0] * W
+        tiem = [0] * W
         tot = [0.0] * W
         for l in range(W):
             run = 0.0
             for k in range(P):
                 X = ldexp(sg * x[l][k], 53 - e)
-                bad = not (abs(X) < 2.0 ** 51) or (X - math.floor(X)) == 0.5
-                badm[l] |= int(bad) << k
-                run = run + (0.0 if bad else rint(X))
+                big = not (abs(X) < 2.0 ** 51)
+                tie = (not big) and (X - math.floor(X)) == 0.5
+                bigm[l] |= int(big) << k
+                tiem[l] |= int(tie) << k
+                # a tie counts its lower neighbour floor(X); the parity pass below adds 1 when it rounds up
+                run = run + (0.0 if big else (float(math.floor(X)) if tie else rint(X)))
                 L[l][k] = run
             tot[l] = run
-        # exclusive scan (exact for lanes up to the first exit in the model as on the GPU)
         E = [0.0] * W
         s = 0.0
         for l in range(W):
             E[l] = s
             s = s + tot[l]
-        outm = [0] * W
+        T = [[A + (E[l] + L[l][k]) for k in range(P)] for l in range(W)]
+        # hard exits: large elements or prefixes near the binade ends (a margin of
+        # MARGIN grid steps absorbs the tie corrections, at most MAXTIE of them)
+        MARGIN, MAXTIE = 64, 32
+        fh = c
         for l in range(W):
             kl = min(max(c - P * l, 0), P)
-            for k in range(P):
-                T = A + (E[l] + L[l][k])
-                out = k < kl and (((badm[l] >> k) & 1) or not (2.0 ** 52 + 1 <= T <= 2.0 ** 53 - 1))
-                outm[l] |= int(out) << k
-        lanes = [l for l in range(W) if outm[l]]
-        if not lanes:
+            for k in range(kl):
+                if ((bigm[l] >> k) & 1) or not (2.0 ** 52 + MARGIN <= T[l][k] <= 2.0 ** 53 - MARGIN):
+                    fh = min(fh, P * l + k)
+        # ties before the first hard exit, in order: round half to even
+        nt = 0
+        for q in range(fh):
+            l, k = divmod(q, P)
+            if (tiem[l] >> k) & 1:
+                if nt == MAXTIE:
+                    fh = q  # too many: this tie is added for real
+                    break
+                nt += 1
+                stats["ties"] += 1
+                if int(T[l][k]) & 1:
+                    for p2 in range(q, W * P):
+                        l2, k2 = divmod(p2, P)
+                        T[l2][k2] += 1.0
+        if fh == c:
             ll, kk = (c - 1) // P, (c - 1) % P
-            acc = sg * ldexp(A + (E[ll] + L[ll][kk]), e - 53)
+            acc = sg * ldexp(T[ll][kk], e - 53)
             i += c
         else:
-            lf = lanes[0]
-            fk = (outm[lf] & -outm[lf]).bit_length() - 1
-            Tpre = A + E[lf] if fk == 0 else A + (E[lf] + L[lf][fk - 1])
+            lf, fk = divmod(fh, P)
+            Tpre = A if fh == 0 else T[(fh - 1) // P][(fh - 1) % P]
             acc = sg * ldexp(Tpre, e - 53)
             acc = acc + x[lf][fk]
-            f = P * lf + fk
+            f = fh
             i += f + 1
             stats["exits"] += 1
             if f < 16:
@@ -102,7 +121,7 @@ def check(seed=1, trials=3000):
     """Returns (cases, stats) or raises AssertionError on the first mismatch."""
     rnd = random.Random(seed)
     cases = 0
-    st = {"steps": 0, "exits": 0, "seq": 0}
+    st = {"steps": 0, "exits": 0, "seq": 0, "ties": 0}
     for trial in range(trials):
         kind = trial % 6
         n = rnd.choice([0, 1, 5, 63, 64, 65, 255, 256, 257, 286, 600, 1300])
@@ -132,7 +151,8 @@ def check(seed=1, trials=3000):
 
 def main():
     cases, st = check(int(sys.argv[1]) if len(sys.argv) > 1 else 1)
-    print(f"ok: {cases} cases, {st['steps']} steps, {st['exits']} exits, {st['seq']} sequential elements")
+    print(f"ok: {cases} cases, {st['steps']} steps, {st['exits']} exits, {st['ties']} ties in-scan, "
+          f"{st['seq']} sequential elements")
     return 0
 
 
