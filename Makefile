@@ -46,7 +46,7 @@ clean:
 # Phase-timing build of the partitioned cooperative kernel and the fused
 # k-means (s_memtime stamps, kml_debug_part_stamps / kml_debug_km_stamps);
 # load it with KML_LIB=kmldpc_amd/libkmldpc_amd_stamps.so
-STAMPED  := bp_coop kmeans
+STAMPED  := bp_coop kmeans bp_regular
 STAMPS_LIB := kmldpc_amd/libkmldpc_amd_stamps.so
 STAMPS_OBJS := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(CPP_SRCS) $(filter-out $(STAMPED),$(HIP_SRCS)))) \
                $(addprefix $(OBJDIR)/stamps/,$(addsuffix .o,$(STAMPED)))

@@ -42,6 +42,30 @@ namespace {
 
 constexpr int kRedBytes = 16;
 
+// Phase timing (stamps build, -DKML_STAMPS=1; tools/reg_stamps.py): thread 0's
+// s_memtime deltas summed per workgroup in registers, flushed at the end:
+// [0] queue + barrier, [1] demap / P0, [2] priors + barrier, [3] iterations,
+// [4] epilogue (outputs, counts) + barrier, [5] result atomics, [6] codewords,
+// [7] iterations run (CN phases).
+#ifndef KML_STAMPS
+#define KML_STAMPS 0
+#endif
+#if KML_STAMPS
+__device__ unsigned long long kml_reg_stamps[8];
+#define REG_STAMP(i)                                               \
+  do {                                                             \
+    if (tid == 0) {                                                \
+      const unsigned long long _t = __builtin_amdgcn_s_memtime();  \
+      rs_acc[(i)] += _t - rs_prev;                                 \
+      rs_prev = _t;                                                \
+    }                                                              \
+  } while (0)
+#else
+#define REG_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 // swap a double with the adjacent lane (quad_perm [1,0,3,2])
 __device__ __forceinline__ double swap_pair(double x) {
   const int lo = __double2loint(x), hi = __double2hiint(x);
@@ -73,11 +97,14 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
     // their dependent fma / rcp sequences overlap.  On the FAST path the
     // boundary state beta = (1, 1) is applied as the identity (x * 1.0 == x).
     {
+      // InitMsg (binaryldpccodec.cc:166-170): every c2v is 0.5 before the
+      // first CN phase, so iteration 0 takes the constant instead of slots
+      // initialised in LDS (every slot is written before it is read)
       double c0s[RV][DV];
 #pragma unroll
       for (int r = 0; r < RV; ++r)
 #pragma unroll
-        for (int k = 0; k < DV; ++k) c0s[r][k] = lds_ld<double>(vaddr[r][k]);
+        for (int k = 0; k < DV; ++k) c0s[r][k] = iter == 0 ? 0.5 : lds_ld<double>(vaddr[r][k]);
       double a0[RV], a1[RV], al0[RV][DV], al1[RV][DV];
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
@@ -246,7 +273,6 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
   constexpr int H = (DC + 1) / 2;
   const int tid = threadIdx.x;
   const int odd = tid & 1;
-  double2 *slots = reinterpret_cast<double2 *>(smem);
   int *red = reinterpret_cast<int *>(smem + (size_t)c.E * 16);
   unsigned char *cch = smem + (size_t)c.E * 16 + kRedBytes;
 
@@ -285,6 +311,9 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
     }
   }
 
+#if KML_STAMPS
+  unsigned long long rs_prev = __builtin_amdgcn_s_memtime(), rs_acc[8] = {};
+#endif
   for (;;) {
     __syncthreads();
     if (tid == 0) {
@@ -294,6 +323,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
     }
     __syncthreads();
     const int entry = red[3];
+    REG_STAMP(0);
     if (entry >= a.B) break;
     const int cw = a.cw_idx ? a.cw_idx[entry] : entry;
     const double *p0;
@@ -315,6 +345,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
       if (a.p0_sel) p0 += (long long)a.p0_sel[cw] * a.p0_sel_stride;
     }
 
+    REG_STAMP(1);
     double pv[RV];
     bool ok = true;
 #pragma unroll
@@ -322,8 +353,8 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
       pv[r] = (vcol[r] >= c.punct) ? p0[vcol[r] - c.punct] : 0.5;
       ok = ok && fast_prior_ok(pv[r]);
     }
-    for (int e = tid; e < c.E; e += T) slots[e] = make_double2(0.5, 0.5);  // InitMsg (either c2v half)
     const bool fast = __syncthreads_and(ok ? 1 : 0) && fast_allowed;
+    REG_STAMP(2);
 
     int iter = 0;
     bool conv = false;
@@ -334,6 +365,13 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
       decode_reg<T, RV, RC, DV, DC, SYN, false>(c, a, cw, smem, cch_a + tid, vaddr, pv, crow, rb, rb2, wb, ccol, odd, iter,
                                                conv);
 
+    REG_STAMP(3);
+#if KML_STAMPS
+    if (tid == 0) {
+      rs_acc[6] += 1;
+      rs_acc[7] += (unsigned long long)iter;
+    }
+#endif
     if (a.iter_count > 0) {
       if (a.uu_hat) {
         uint8_t *u = a.uu_hat + (long long)cw * c.K;
@@ -362,6 +400,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
       }
     }
     __syncthreads();
+    REG_STAMP(4);
     if (tid == 0) {
       if (a.ret) a.ret[cw] = iter + (iter < a.max_iter);
       if (a.parity_cnt) a.parity_cnt[cw] = red[0];
@@ -381,7 +420,12 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
         }
       }
     }
+    REG_STAMP(5);
   }
+#if KML_STAMPS
+  if (tid == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&kml_reg_stamps[i], rs_acc[i]);
+#endif
 }
 
 template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB>
@@ -422,6 +466,19 @@ hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s)
   return a.syn ? launch_reg_t<768, 3, 3, 3, 6, true, 0>(c, a, s, fast)
                : launch_reg_t<768, 3, 3, 3, 6, false, 0>(c, a, s, fast);
 }
+
+#if KML_STAMPS
+}  // namespace kml
+extern "C" int kml_debug_reg_stamps(unsigned long long *out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(kml::kml_reg_stamps), sizeof(kml::kml_reg_stamps));
+  if (reset) {
+    unsigned long long zero[8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(kml::kml_reg_stamps), zero, sizeof(zero));
+  }
+  return e == hipSuccess ? 0 : -3;
+}
+namespace kml {
+#endif
 
 bool bp_regular_fuses_demap(const DevCode &c, int bits) {
   if (const char *e = getenv("KML_FUSED_DEMAP"))
