@@ -46,7 +46,7 @@ clean:
 # Phase-timing build of the partitioned cooperative kernel and the fused
 # k-means (s_memtime stamps, kml_debug_part_stamps / kml_debug_km_stamps);
 # load it with KML_LIB=kmldpc_amd/libkmldpc_amd_stamps.so
-STAMPED  := bp_coop kmeans bp_regular
+STAMPED  := bp_coop kmeans bp_regular bp_irregular
 STAMPS_LIB := kmldpc_amd/libkmldpc_amd_stamps.so
 STAMPS_OBJS := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(CPP_SRCS) $(filter-out $(STAMPED),$(HIP_SRCS)))) \
                $(addprefix $(OBJDIR)/stamps/,$(addsuffix .o,$(STAMPED)))
@@ -57,3 +57,20 @@ $(STAMPS_LIB): $(STAMPS_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(STAMPS_OBJS) -Wl,-rpath,/opt/rocm/lib
 stamps: $(STAMPS_LIB)
 .PHONY: stamps
+
+# Experiment builds of the whole library with extra defines (A/B on one box):
+#   make variant V=<name> VFLAGS="-DKML_IRR_VN_PAIR_MAX=5"  -> kmldpc_amd/libkmldpc_amd_<name>.so
+VAR_DIR  := $(OBJDIR)/var_$(V)
+VAR_OBJS := $(addprefix $(VAR_DIR)/,$(addsuffix .o,$(CPP_SRCS) $(HIP_SRCS)))
+$(VAR_DIR)/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(VAR_DIR)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $@ $<
+$(VAR_DIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(VAR_DIR)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $@ $<
+kmldpc_amd/libkmldpc_amd_$(V).so: $(VAR_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(VAR_OBJS) -Wl,-rpath,/opt/rocm/lib
+variant:
+	@test -n "$(V)" || (echo "variant: set V=<name>" && false)
+	$(MAKE) kmldpc_amd/libkmldpc_amd_$(V).so V=$(V) VFLAGS='$(VFLAGS)'
+.PHONY: variant

@@ -43,6 +43,9 @@ __device__ __forceinline__ double swap_pair(double x) {
   const int hi2 = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
   return __hiloint2double(hi2, lo2);
 }
+__device__ __forceinline__ double with_sign(double x, int bit) {
+  return __hiloint2double((__double2hiint(x) & 0x7FFFFFFF) | (bit << 31), __double2loint(x));
+}
 __device__ __forceinline__ int swap_pair_i(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }
 
 // R columns of degree D (binaryldpccodec.cc:177-213), their chains
@@ -56,6 +59,7 @@ __device__ __forceinline__ void vn_cols(double2 *slots, const unsigned short *co
 #pragma unroll
     for (int k = 0; k < D; ++k) c0s[r][k] = slots[cs[r][k]].x;
   double a0[R], a1[R], al0[R][D], al1[R][D];
+  int hb[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     a0[r] = p[r];
@@ -72,7 +76,7 @@ __device__ __forceinline__ void vn_cols(double2 *slots, const unsigned short *co
       if (k + 1 < D)
         div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r]);
       else
-        *hard[r] = (unsigned char)hard_decision<FAST>(n0, n1);
+        *hard[r] = (unsigned char)(hb[r] = hard_decision<FAST>(n0, n1));
     }
   double b0[R], b1[R];
 #pragma unroll
@@ -89,7 +93,9 @@ __device__ __forceinline__ void vn_cols(double2 *slots, const unsigned short *co
         div2<FAST, true>(t0, t1, t0 + t1, q0, q1);
       else
         div2<FAST>(t0, t1, t0 + t1, q0, q1);
-      slots[cs[r][k]] = make_double2(q0, q1);
+      // the column's decision rides in the sign bit of the v2c q1 (a probability,
+      // so the bit is otherwise clear): the parity check reads it in row order
+      slots[cs[r][k]] = make_double2(q0, with_sign(q1, hb[r]));
       if (k > 0) {
         const double c0 = c0s[r][k];
         if (unit) {  // (c0, 1 - c0) / (c0 + (1 - c0)): the sum rounds to exactly 1 (bp_common.hpp)
@@ -124,7 +130,7 @@ __device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], 
       if (advance) {
         const double2 m = slots[base[r] + (odd ? D - 1 - st : st)];
         m0[r] = m.x;
-        m1[r] = m.y;
+        m1[r] = fabs(m.y);  // clear the decision bit (vn_cols)
       }
     }
 #pragma unroll
@@ -217,43 +223,109 @@ __device__ __forceinline__ void cn_any(int d, double2 *slots, const int (&base)[
   }
 }
 
+// Phase timing (stamps build, -DKML_STAMPS=1; tools/irr_stamps.py): lane 0 of
+// every wave sums its s_memtime deltas per phase of an iteration; the sums are
+// flushed per wave at the end of each codeword: [0] VN paired round, [1] VN
+// single round, [2] VN barrier wait, [3] parity, [4] CN paired round, [5] CN
+// single round, [6] CN barrier wait (+ OR), [7] iterations run.
+#ifndef KML_STAMPS
+#define KML_STAMPS 0
+#endif
+#if KML_STAMPS
+__device__ unsigned long long kml_irr_stamps[kIrrThreads / 64][8];
+#define IRR_STAMP(i)                                               \
+  do {                                                             \
+    if ((threadIdx.x & 63) == 0) {                                 \
+      const unsigned long long _t = __builtin_amdgcn_s_memtime();  \
+      st_acc[(i)] += _t - st_prev;                                 \
+      st_prev = _t;                                                \
+    }                                                              \
+  } while (0)
+#else
+#define IRR_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 // Column / row of the lane in round r of the plan (layout.hpp IrregularPlan):
 // rounds 0 and 1 pair two items of one degree, round 2 holds single items.
 template <int T, bool SYN, bool FAST>
 __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, int cw, double2 *slots,
                                            const unsigned short *cslot, const double *p0s, unsigned char *cch, int odd,
                                            const int (&vcol)[3], const int (&crow)[3], int &iter_out, bool &conv_out) {
+  // Each lane's plan packed into one word per round (slot base | degree << 14
+  // | column or row << 18; ~0 = no item), built once per codeword: the
+  // iteration loop makes no global loads.  The words are laundered at the top
+  // of every iteration so that nothing derived from them is loop-invariant
+  // (left invariant, LICM hoists per-degree offsets out of the loop and spills).
+  unsigned vpk[3], cpk[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    vpk[r] = ~0u;
+    cpk[r] = ~0u;
+    if (vcol[r] >= 0) {
+      const int b = c.col_ptr[vcol[r]];
+      vpk[r] = (unsigned)b | (unsigned)(c.col_ptr[vcol[r] + 1] - b) << 14 | (unsigned)vcol[r] << 18;
+    }
+    if (crow[r] >= 0) {
+      const int b = c.row_ptr[crow[r]];
+      cpk[r] = (unsigned)b | (unsigned)(c.row_ptr[crow[r] + 1] - b) << 14 | (unsigned)crow[r] << 18;
+    }
+  }
+  auto pbase = [](unsigned w) { return (int)(w & 0x3FFFu); };
+  auto pdeg = [](unsigned w) { return (int)((w >> 14) & 15u); };
+  auto pitem = [](unsigned w) { return (int)(w >> 18); };
   int iter = 0;
   bool conv = false;
   auto prior = [&](int v) { return v >= c.punct ? p0s[v - c.punct] : 0.5; };  // :126-134
+#if KML_STAMPS
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
+#endif
   for (; iter < a.iter_count; ++iter) {
+    IRR_STAMP(6);
+    unsigned vp[3], cp[3];
+    int od = odd;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      vp[r] = vpk[r];
+      cp[r] = cpk[r];
+      asm volatile("" : "+v"(vp[r]), "+v"(cp[r]));
+    }
+    asm volatile("" : "+v"(od));
     set_prio(3);
-    if (vcol[0] >= 0) {  // paired round: two columns of one degree, interleaved
-      const int b0 = c.col_ptr[vcol[0]], b1 = c.col_ptr[vcol[1]];
-      const unsigned short *const cs[2] = {cslot + b0, cslot + b1};
-      const double p[2] = {prior(vcol[0]), prior(vcol[1])};
-      unsigned char *const h[2] = {&cch[vcol[0]], &cch[vcol[1]]};
-      vn_any<2, FAST>(c.col_ptr[vcol[0] + 1] - b0, slots, cs, p, h);
+    if (vp[0] != ~0u) {  // paired round: two columns of one degree, interleaved
+      const int v0 = pitem(vp[0]), v1 = pitem(vp[1]);
+      const unsigned short *const cs[2] = {cslot + pbase(vp[0]), cslot + pbase(vp[1])};
+      const double p[2] = {prior(v0), prior(v1)};
+      unsigned char *const h[2] = {&cch[v0], &cch[v1]};
+      vn_any<2, FAST>(pdeg(vp[0]), slots, cs, p, h);
     }
+    IRR_STAMP(0);
     set_prio(1);
-    if (vcol[2] >= 0) {
-      const int b = c.col_ptr[vcol[2]];
-      const unsigned short *const cs[1] = {cslot + b};
-      const double p[1] = {prior(vcol[2])};
-      unsigned char *const h[1] = {&cch[vcol[2]]};
-      vn_any<1, FAST>(c.col_ptr[vcol[2] + 1] - b, slots, cs, p, h);
+    if (vp[2] != ~0u) {
+      const int v = pitem(vp[2]);
+      const unsigned short *const cs[1] = {cslot + pbase(vp[2])};
+      const double p[1] = {prior(v)};
+      unsigned char *const h[1] = {&cch[v]};
+      vn_any<1, FAST>(pdeg(vp[2]), slots, cs, p, h);
     }
+    IRR_STAMP(1);
     __syncthreads();
+    IRR_STAMP(2);
 
+    // parity of the row halves from the decisions the VN phase left in the
+    // sign bits of the row's own slots (no column indirection)
     int fail = 0;
-#pragma unroll 1
+#pragma unroll
     for (int r = 0; r < 3; ++r) {
       int p = 0, d = 0;
-      if (crow[r] >= 0) {
-        const int base = c.row_ptr[crow[r]];
-        d = c.row_ptr[crow[r] + 1] - base;
-        const int lo = odd ? (d + 1) / 2 : 0, hi = odd ? d : (d + 1) / 2;
-        for (int k = lo; k < hi; ++k) p ^= cch[c.row_col[base + k]];
+      if (cp[r] != ~0u) {
+        const int base = pbase(cp[r]);
+        d = pdeg(cp[r]);
+        const int lo = od ? (d + 1) / 2 : 0, hi = od ? d : (d + 1) / 2;
+        const unsigned *hw = reinterpret_cast<const unsigned *>(slots) + 3;  // high word of slot.y
+        for (int k = lo; k < hi; ++k) p ^= hw[4 * (base + k)];
+        p = (unsigned)p >> 31;
       }
       const int full = p ^ swap_pair_i(p);
       if (d > 0) fail |= full;
@@ -262,21 +334,24 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
     // (speculative CN, as in bp_regular.hip); syndromes are kept until the
     // phase is known to count
     double sv[3] = {0.0, 0.0, 0.0};
+    IRR_STAMP(3);
     set_prio(2);
-    if (crow[0] >= 0) {  // both lanes of a pair agree
-      const int base[2] = {c.row_ptr[crow[0]], c.row_ptr[crow[1]]};
+    if (cp[0] != ~0u) {  // both lanes of a pair agree
+      const int base[2] = {pbase(cp[0]), pbase(cp[1])};
       double s2[2];
-      cn_any<2, SYN, FAST>(c.row_ptr[crow[0] + 1] - base[0], slots, base, odd, s2);
+      cn_any<2, SYN, FAST>(pdeg(cp[0]), slots, base, od, s2);
       sv[0] = s2[0];
       sv[1] = s2[1];
     }
+    IRR_STAMP(4);
     set_prio(0);
-    if (crow[2] >= 0) {
-      const int base[1] = {c.row_ptr[crow[2]]};
+    if (cp[2] != ~0u) {
+      const int base[1] = {pbase(cp[2])};
       double s1[1];
-      cn_any<1, SYN, FAST>(c.row_ptr[crow[2] + 1] - base[0], slots, base, odd, s1);
+      cn_any<1, SYN, FAST>(pdeg(cp[2]), slots, base, od, s1);
       sv[2] = s1[0];
     }
+    IRR_STAMP(5);
     if (!__syncthreads_or(fail)) {
       conv = true;
       break;
@@ -284,9 +359,16 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
     if constexpr (SYN) {
 #pragma unroll
       for (int r = 0; r < 3; ++r)
-        if (crow[r] >= 0 && !odd) a.syn[(long long)cw * c.M + crow[r]] = sv[r];  // alpha past the last edge (:274)
+        if (cp[r] != ~0u && !od) a.syn[(long long)cw * c.M + pitem(cp[r])] = sv[r];  // alpha past the last edge (:274)
     }
   }
+  IRR_STAMP(6);
+#if KML_STAMPS
+  if ((threadIdx.x & 63) == 0) {
+    st_acc[7] = iter;
+    for (int i = 0; i < 8; ++i) atomicAdd(&kml_irr_stamps[threadIdx.x >> 6][i], st_acc[i]);
+  }
+#endif
   iter_out = iter;
   conv_out = conv;
 }
@@ -415,3 +497,14 @@ hipError_t launch_bp_irregular(const DevCode &c, const BpLaunch &a, hipStream_t 
 }
 
 }  // namespace kml
+
+#if KML_STAMPS
+extern "C" int kml_debug_irr_stamps(unsigned long long *out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(kml::kml_irr_stamps), sizeof(kml::kml_irr_stamps));
+  if (reset) {
+    unsigned long long zero[sizeof(kml::kml_irr_stamps) / 8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(kml::kml_irr_stamps), zero, sizeof(zero));
+  }
+  return e == hipSuccess ? 0 : -3;
+}
+#endif

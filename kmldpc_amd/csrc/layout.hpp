@@ -88,8 +88,14 @@ namespace kml {
 // the 4 SIMDs (wave w runs on SIMD w % 4) is balanced.  Any placement gives
 // the same decoder output: it only moves work between lanes.
 constexpr int kIrrThreads = 768;  // threads per workgroup of bp_irregular.hip (its plan is made for this)
-constexpr int kIrrVnPairMax = 4;  // highest column degree bp_irregular.hip pairs
-constexpr int kIrrCnPairMax = 8;  // highest row degree it pairs (BG2, 50 iterations: 4/8 19.7 ms,
+#ifndef KML_IRR_VN_PAIR_MAX  // overridable for experiment builds (Makefile "variant")
+#define KML_IRR_VN_PAIR_MAX 4
+#endif
+#ifndef KML_IRR_CN_PAIR_MAX
+#define KML_IRR_CN_PAIR_MAX 8
+#endif
+constexpr int kIrrVnPairMax = KML_IRR_VN_PAIR_MAX;  // highest column degree bp_irregular.hip pairs
+constexpr int kIrrCnPairMax = KML_IRR_CN_PAIR_MAX;  // highest row degree it pairs (BG2, 50 iterations: 4/8 19.7 ms,
                                   // 5/8 20.5, 7/8 21.8, 9/8 23.0 with c2v reloads against spills)
 
 struct IrregularPlan {
