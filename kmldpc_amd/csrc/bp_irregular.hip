@@ -128,7 +128,7 @@ __device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], 
     for (int r = 0; r < R; ++r) {
       m0[r] = m1[r] = 0.0;
       if (advance) {
-        const double2 m = slots[base[r] + (odd ? D - 1 - st : st)];
+        const double2 m = slots[base[r] + (odd ? D - 1 - st : st) * kIrrCnStride];
         m0[r] = m.x;
         m1[r] = fabs(m.y);  // clear the decision bit (vn_cols)
       }
@@ -144,7 +144,7 @@ __device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], 
         const double t0 = s0[r] * y0 + s1[r] * y1;
         const double t1 = s0[r] * y1 + s1[r] * y0;
         const double q = clip_c2v<FAST>(div1<FAST, true>(t0, t0 + t1));
-        if (!odd) slots[base[r] + st].x = q;
+        if (!odd) slots[base[r] + st * kIrrCnStride].x = q;
       }
       if (st >= S) {
         // c2v of edge (odd ? st : D-1-st) from (own state at D-1-st, partner state now)
@@ -153,7 +153,7 @@ __device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], 
         const bool unit = FAST && st == D - 1;  // own state is the boundary (1, 0)
         const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
         const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
-        slots[base[r] + (odd ? st : D - 1 - st)].x = clip_c2v<FAST>(div1<FAST, true>(t0, t0 + t1));
+        slots[base[r] + (odd ? st : D - 1 - st) * kIrrCnStride].x = clip_c2v<FAST>(div1<FAST, true>(t0, t0 + t1));
       }
     }
     if (advance) {
@@ -268,8 +268,9 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
       vpk[r] = (unsigned)b | (unsigned)(c.col_ptr[vcol[r] + 1] - b) << 14 | (unsigned)vcol[r] << 18;
     }
     if (crow[r] >= 0) {
-      const int b = c.row_ptr[crow[r]];
-      cpk[r] = (unsigned)b | (unsigned)(c.row_ptr[crow[r] + 1] - b) << 14 | (unsigned)crow[r] << 18;
+      const int b = c.irr_cn_base[r * (T / 2) + (threadIdx.x >> 1)];
+      const int d = c.row_ptr[crow[r] + 1] - c.row_ptr[crow[r]];
+      cpk[r] = (unsigned)b | (unsigned)d << 14 | (unsigned)crow[r] << 18;
     }
   }
   auto pbase = [](unsigned w) { return (int)(w & 0x3FFFu); };
@@ -324,7 +325,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
         d = pdeg(cp[r]);
         const int lo = od ? (d + 1) / 2 : 0, hi = od ? d : (d + 1) / 2;
         const unsigned *hw = reinterpret_cast<const unsigned *>(slots) + 3;  // high word of slot.y
-        for (int k = lo; k < hi; ++k) p ^= hw[4 * (base + k)];
+        for (int k = lo; k < hi; ++k) p ^= hw[4 * (base + k * kIrrCnStride)];
         p = (unsigned)p >> 31;
       }
       const int full = p ^ swap_pair_i(p);
@@ -379,12 +380,13 @@ __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, 
   const int tid = threadIdx.x;
   const int odd = tid & 1;
   double2 *slots = reinterpret_cast<double2 *>(smem);
-  double *p0s = reinterpret_cast<double *>(smem + (size_t)c.E * 16);
-  unsigned short *cslot = reinterpret_cast<unsigned short *>(smem + (size_t)c.E * 16 + (size_t)c.cc_len * 8);
-  int *red = reinterpret_cast<int *>(smem + (size_t)c.E * 18 + (size_t)c.cc_len * 8);
-  unsigned char *cch = smem + (size_t)c.E * 18 + (size_t)c.cc_len * 8 + kRedBytes;
+  const size_t sb = (size_t)c.irr_slots * 16;  // slot blocks (layout.hpp kIrrCnStride)
+  double *p0s = reinterpret_cast<double *>(smem + sb);
+  unsigned short *cslot = reinterpret_cast<unsigned short *>(smem + sb + (size_t)c.cc_len * 8);
+  int *red = reinterpret_cast<int *>(smem + sb + (size_t)c.E * 2 + (size_t)c.cc_len * 8);
+  unsigned char *cch = smem + sb + (size_t)c.E * 2 + (size_t)c.cc_len * 8 + kRedBytes;
 
-  for (int e = tid; e < c.E; e += T) cslot[e] = (unsigned short)c.col_slot[e];
+  for (int e = tid; e < c.E; e += T) cslot[e] = (unsigned short)c.irr_col_slot[e];
   int vcol[3], crow[3];
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
@@ -412,7 +414,7 @@ __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, 
       p0s[i] = q;
       ok = ok && fast_prior_ok(q);
     }
-    for (int e = tid; e < c.E; e += T) slots[e].x = 0.5;  // InitMsg
+    for (int e = tid; e < c.irr_slots; e += T) slots[e].x = 0.5;  // InitMsg
     const bool fast = __syncthreads_and(ok ? 1 : 0) && fast_allowed;
 
     int iter = 0;
@@ -469,10 +471,14 @@ __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, 
   }
 }
 
+size_t irr_lds_bytes(const DevCode &c) {
+  return (size_t)c.irr_slots * 16 + (size_t)c.E * 2 + (size_t)c.cc_len * 8 + kRedBytes + (size_t)c.N;
+}
+
 template <int T, bool SYN>
 hipError_t launch_irr_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
   auto kern = bp_irregular_kernel<T, SYN>;
-  const size_t lds = (size_t)c.E * 18 + (size_t)c.cc_len * 8 + kRedBytes + (size_t)c.N;
+  const size_t lds = irr_lds_bytes(c);
   hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   int dev = 0, ncu = 0;
@@ -490,7 +496,7 @@ hipError_t launch_irr_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int 
 
 hipError_t launch_bp_irregular(const DevCode &c, const BpLaunch &a, hipStream_t s) {
   constexpr int T = kIrrThreads;
-  if ((long long)c.E * 18 + 8LL * c.cc_len + kRedBytes + c.N > 160 * 1024 || c.E > 65535) return hipErrorNotSupported;
+  if (irr_lds_bytes(c) > 160 * 1024 || c.irr_slots > 16383) return hipErrorNotSupported;
   if (!c.irr_ok || !c.irr_vn) return hipErrorNotSupported;
   const int fast = c.dv_max <= kFastMaxColumnDegree ? 1 : 0;
   return a.syn ? launch_irr_t<T, true>(c, a, s, fast) : launch_irr_t<T, false>(c, a, s, fast);

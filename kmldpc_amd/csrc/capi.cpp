@@ -178,6 +178,8 @@ int upload_code(kml_ctx *c) {
     irr = kml::IrregularPlan();
   reserve(irr.vn.size() * 4);
   reserve(irr.cn.size() * 4);
+  reserve(irr.cn_base.size() * 4);
+  reserve(irr.col_slot.size() * 4);
   HIPCHK(c, c->d_graph.ensure(bytes), "hipMalloc(graph)");
   std::vector<unsigned char> host(bytes, 0);
   auto put = [&](int i, const void *src, size_t n) {
@@ -204,6 +206,8 @@ int upload_code(kml_ctx *c) {
   put(18, part.rx.data(), part.rx.size() * 4);
   put(19, irr.vn.data(), irr.vn.size() * 4);
   put(20, irr.cn.data(), irr.cn.size() * 4);
+  put(21, irr.cn_base.data(), irr.cn_base.size() * 4);
+  put(22, irr.col_slot.data(), irr.col_slot.size() * 4);
   HIPCHK(c, hipMemcpy(c->d_graph.p, host.data(), bytes, hipMemcpyHostToDevice), "upload graph");
   unsigned char *base = c->d_graph.as<unsigned char>();
   kml::DevCode &d = c->dc;
@@ -229,6 +233,9 @@ int upload_code(kml_ctx *c) {
   d.pt_rx = part.G ? reinterpret_cast<const int32_t *>(base + off[18]) : nullptr;
   d.irr_vn = irr.vn.empty() ? nullptr : reinterpret_cast<const int32_t *>(base + off[19]);
   d.irr_cn = irr.cn.empty() ? nullptr : reinterpret_cast<const int32_t *>(base + off[20]);
+  d.irr_cn_base = irr.cn.empty() ? nullptr : reinterpret_cast<const int32_t *>(base + off[21]);
+  d.irr_col_slot = irr.cn.empty() ? nullptr : reinterpret_cast<const int32_t *>(base + off[22]);
+  d.irr_slots = irr.n_slots;
   d.pt_ncut = part.ncut;
   d.pt_mirror = part.mirror_max;
   for (int m = 0; m < 4; m++) {

@@ -26,7 +26,8 @@ struct DevCode {
   int regular;  // every column has degree dv_max and every row dc_max
   int irr_ok;   // column degrees in [1, 9] and row degrees in [2, 10] (bp_irregular.hip)
   // Round plan of bp_irregular.hip (layout.hpp IrregularPlan); null when none fits.
-  const int32_t *irr_vn, *irr_cn;
+  const int32_t *irr_vn, *irr_cn, *irr_cn_base, *irr_col_slot;
+  int irr_slots;
   // LDS placement plan of bp_regular.hip (layout.hpp); null when the code does
   // not take that kernel.  vn_order then holds the planned column order.
   const int32_t *reg_c2v;  // aligned with col_slot: byte offset of the c2v message

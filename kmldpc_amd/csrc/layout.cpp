@@ -465,6 +465,32 @@ bool plan_irregular(const LdpcCode &L, int T, int vn_pair_max, int cn_pair_max, 
     if (cs_of[w] >= 0)
       for (size_t l = 0; l < cs[cs_of[w]].a.size(); ++l) out.cn[T + w * 32 + l] = cs[cs_of[w]].a[l];
   }
+  // slot blocks (kIrrCnStride), one per wave and round, in plan order
+  std::vector<int32_t> slot_of(L.E, -1);
+  out.cn_base.assign(3 * T / 2, -1);
+  int next = 0;
+  for (int r = 0; r < 3; ++r)
+    for (int w = 0; w < W; ++w) {
+      const int p0 = r * (T / 2) + w * 32;
+      int dw = 0;
+      for (int pi = 0; pi < 32; ++pi) {
+        const int row = out.cn[p0 + pi];
+        if (row >= 0) dw = std::max(dw, L.row_ptr[row + 1] - L.row_ptr[row]);
+      }
+      for (int pi = 0; pi < 32; ++pi) {
+        const int row = out.cn[p0 + pi];
+        if (row < 0) continue;
+        out.cn_base[p0 + pi] = next + pi;
+        for (int e = L.row_ptr[row]; e < L.row_ptr[row + 1]; ++e)
+          slot_of[e] = next + pi + (e - L.row_ptr[row]) * kIrrCnStride;
+      }
+      next += dw * kIrrCnStride;
+    }
+  for (int32_t s : slot_of)
+    if (s < 0) return false;
+  out.n_slots = next;
+  out.col_slot.resize(L.E);
+  for (int e = 0; e < L.E; ++e) out.col_slot[e] = slot_of[L.col_slot[e]];
   return true;
 }
 

@@ -98,9 +98,19 @@ constexpr int kIrrVnPairMax = KML_IRR_VN_PAIR_MAX;  // highest column degree bp_
 constexpr int kIrrCnPairMax = KML_IRR_CN_PAIR_MAX;  // highest row degree it pairs (BG2, 50 iterations: 4/8 19.7 ms,
                                   // 5/8 20.5, 7/8 21.8, 9/8 23.0 with c2v reloads against spills)
 
+// Slot layout of the irregular kernel: the rows of a wave's round (32 lane
+// pairs, one degree) form a block in which edge e of the row at pair index pi
+// sits at slot pi + e * kIrrCnStride, so at every CN step a wave reads two
+// contiguous 512-byte runs (conflict-free b128 reads) instead of 32 rows
+// strided by their degree.
+constexpr int kIrrCnStride = 32;
+
 struct IrregularPlan {
-  std::vector<int32_t> vn;  // [3*T]: column of position r*T + t, -1 = idle
-  std::vector<int32_t> cn;  // [3*T/2]: row of lane pair r*T/2 + (t >> 1), -1 = idle
+  std::vector<int32_t> vn;        // [3*T]: column of position r*T + t, -1 = idle
+  std::vector<int32_t> cn;        // [3*T/2]: row of lane pair r*T/2 + (t >> 1), -1 = idle
+  std::vector<int32_t> cn_base;   // [3*T/2]: slot of edge 0 of that row, -1 = idle
+  std::vector<int32_t> col_slot;  // [E]: slot of each column-ordered edge (as LdpcCode::col_slot)
+  int n_slots = 0;                // slots incl. the holes of partly filled blocks
 };
 
 // False when the code's degree groups do not fit three rounds of T lanes.

@@ -97,7 +97,23 @@ static void check_irregular(const LdpcCode &L) {
       CHECK(row_deg(L, a) <= kIrrCnPairMax, "pair %d row degree %d", q, row_deg(L, a));
     }
   }
-  printf("irregular: plan ok for T=%d\n", T);
+  // slot blocks: edge e of the row at a lane pair sits at cn_base + e * kIrrCnStride,
+  // every edge has its own slot, and the column-ordered table points at the same slots
+  CHECK((int)P.cn_base.size() == 3 * T / 2 && (int)P.col_slot.size() == L.E, "slot table sizes");
+  std::vector<int> owner(P.n_slots, -1), slot_of(L.E, -1);
+  for (int q = 0; q < 3 * T / 2; q++) {
+    const int r = P.cn[q];
+    CHECK((r < 0) == (P.cn_base[q] < 0), "pair position %d base", q);
+    if (r < 0) continue;
+    for (int e = L.row_ptr[r]; e < L.row_ptr[r + 1]; e++) {
+      const int s = P.cn_base[q] + (e - L.row_ptr[r]) * kIrrCnStride;
+      CHECK(s >= 0 && s < P.n_slots && owner[s] < 0, "edge %d slot %d", e, s);
+      if (s >= 0 && s < P.n_slots) owner[s] = e;
+      slot_of[e] = s;
+    }
+  }
+  for (int e = 0; e < L.E; e++) CHECK(P.col_slot[e] == slot_of[L.col_slot[e]], "column edge %d slot", e);
+  printf("irregular: plan ok for T=%d, %d slots for %d edges\n", T, P.n_slots, L.E);
 }
 
 // bp_part_kernel: members own whole column / row blocks; every edge's LDS
