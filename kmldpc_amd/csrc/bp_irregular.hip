@@ -110,15 +110,20 @@ __device__ __forceinline__ void vn_cols(double2 *slots, const unsigned short *co
 
 // Half of R check rows of degree D (binaryldpccodec.cc:235-275), streamed step
 // by step with the R rows interleaved; sv[r] = the forward state past the
-// last edge (syndrom_soft, read on the even lane) when SYN.
+// last edge (syndrom_soft, read on the even lane) when SYN.  par[r] (bit 31)
+// = the XOR of the decisions (vn_cols' sign bits) of the lane's half of the
+// row, from the words the chain loads anyway: the even lane's edges
+// [0, (D+1)/2), the odd lane's [(D+1)/2, D).
 template <int D, int R, bool SYN, bool FAST>
-__device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], int odd, double (&sv)[R]) {
+__device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], int odd, double (&sv)[R],
+                                          unsigned (&par)[R]) {
   constexpr int S = (D + 1) / 2;  // states kept: x[0..S)
   double x0[R][S], x1[R][S], s0[R], s1[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     s0[r] = 1.0;
     s1[r] = 0.0;
+    par[r] = 0;
   }
 #pragma unroll
   for (int st = 0; st < D; ++st) {
@@ -129,6 +134,7 @@ __device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], 
       m0[r] = m1[r] = 0.0;
       if (advance) {
         const double2 m = slots[base[r] + (odd ? D - 1 - st : st) * kIrrCnStride];
+        if (st < D - S || (st < S && !odd)) par[r] ^= (unsigned)__double2hiint(m.y);
         m0[r] = m.x;
         m1[r] = fabs(m.y);  // clear the decision bit (vn_cols)
       }
@@ -205,21 +211,23 @@ __device__ __forceinline__ void vn_any(int d, double2 *slots, const unsigned sho
 }
 
 template <int D, int R, bool SYN, bool FAST>
-__device__ __forceinline__ void cn_halves_if(double2 *slots, const int (&base)[R], int odd, double (&sv)[R]) {
-  if constexpr (R == 1 || D <= kIrrCnPairMax) cn_halves<D, R, SYN, FAST>(slots, base, odd, sv);
+__device__ __forceinline__ void cn_halves_if(double2 *slots, const int (&base)[R], int odd, double (&sv)[R],
+                                             unsigned (&par)[R]) {
+  if constexpr (R == 1 || D <= kIrrCnPairMax) cn_halves<D, R, SYN, FAST>(slots, base, odd, sv, par);
 }
 template <int R, bool SYN, bool FAST>
-__device__ __forceinline__ void cn_any(int d, double2 *slots, const int (&base)[R], int odd, double (&sv)[R]) {
+__device__ __forceinline__ void cn_any(int d, double2 *slots, const int (&base)[R], int odd, double (&sv)[R],
+                                       unsigned (&par)[R]) {
   switch (d) {
-    case 2: cn_halves_if<2, R, SYN, FAST>(slots, base, odd, sv); break;
-    case 3: cn_halves_if<3, R, SYN, FAST>(slots, base, odd, sv); break;
-    case 4: cn_halves_if<4, R, SYN, FAST>(slots, base, odd, sv); break;
-    case 5: cn_halves_if<5, R, SYN, FAST>(slots, base, odd, sv); break;
-    case 6: cn_halves_if<6, R, SYN, FAST>(slots, base, odd, sv); break;
-    case 7: cn_halves_if<7, R, SYN, FAST>(slots, base, odd, sv); break;
-    case 8: cn_halves_if<8, R, SYN, FAST>(slots, base, odd, sv); break;
-    case 9: cn_halves_if<9, R, SYN, FAST>(slots, base, odd, sv); break;
-    default: cn_halves_if<10, R, SYN, FAST>(slots, base, odd, sv); break;
+    case 2: cn_halves_if<2, R, SYN, FAST>(slots, base, odd, sv, par); break;
+    case 3: cn_halves_if<3, R, SYN, FAST>(slots, base, odd, sv, par); break;
+    case 4: cn_halves_if<4, R, SYN, FAST>(slots, base, odd, sv, par); break;
+    case 5: cn_halves_if<5, R, SYN, FAST>(slots, base, odd, sv, par); break;
+    case 6: cn_halves_if<6, R, SYN, FAST>(slots, base, odd, sv, par); break;
+    case 7: cn_halves_if<7, R, SYN, FAST>(slots, base, odd, sv, par); break;
+    case 8: cn_halves_if<8, R, SYN, FAST>(slots, base, odd, sv, par); break;
+    case 9: cn_halves_if<9, R, SYN, FAST>(slots, base, odd, sv, par); break;
+    default: cn_halves_if<10, R, SYN, FAST>(slots, base, odd, sv, par); break;
   }
 }
 
@@ -314,43 +322,41 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
     __syncthreads();
     IRR_STAMP(2);
 
-    // parity of the row halves from the decisions the VN phase left in the
-    // sign bits of the row's own slots (no column indirection)
-    int fail = 0;
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      int p = 0, d = 0;
-      if (cp[r] != ~0u) {
-        const int base = pbase(cp[r]);
-        d = pdeg(cp[r]);
-        const int lo = od ? (d + 1) / 2 : 0, hi = od ? d : (d + 1) / 2;
-        const unsigned *hw = reinterpret_cast<const unsigned *>(slots) + 3;  // high word of slot.y
-        for (int k = lo; k < hi; ++k) p ^= hw[4 * (base + k * kIrrCnStride)];
-        p = (unsigned)p >> 31;
-      }
-      const int full = p ^ swap_pair_i(p);
-      if (d > 0) fail |= full;
-    }
-    // the OR over the workgroup is folded into the CN phase's closing barrier
+    // The early-stop parity of each row comes out of the CN pass (the row
+    // halves' decisions ride in the v2c sign bits the chains load); the OR
+    // over the workgroup is folded into the CN phase's closing barrier
     // (speculative CN, as in bp_regular.hip); syndromes are kept until the
-    // phase is known to count
+    // phase is known to count.
     double sv[3] = {0.0, 0.0, 0.0};
+    unsigned par[3] = {0u, 0u, 0u};
     IRR_STAMP(3);
     set_prio(2);
     if (cp[0] != ~0u) {  // both lanes of a pair agree
       const int base[2] = {pbase(cp[0]), pbase(cp[1])};
       double s2[2];
-      cn_any<2, SYN, FAST>(pdeg(cp[0]), slots, base, od, s2);
+      unsigned p2[2];
+      cn_any<2, SYN, FAST>(pdeg(cp[0]), slots, base, od, s2, p2);
       sv[0] = s2[0];
       sv[1] = s2[1];
+      par[0] = p2[0];
+      par[1] = p2[1];
     }
     IRR_STAMP(4);
     set_prio(0);
     if (cp[2] != ~0u) {
       const int base[1] = {pbase(cp[2])};
       double s1[1];
-      cn_any<1, SYN, FAST>(pdeg(cp[2]), slots, base, od, s1);
+      unsigned p1[1];
+      cn_any<1, SYN, FAST>(pdeg(cp[2]), slots, base, od, s1, p1);
       sv[2] = s1[0];
+      par[2] = p1[0];
+    }
+    int fail = 0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int p = (int)(par[r] >> 31);
+      const int full = p ^ swap_pair_i(p);
+      if (cp[r] != ~0u) fail |= full;
     }
     IRR_STAMP(5);
     if (!__syncthreads_or(fail)) {
