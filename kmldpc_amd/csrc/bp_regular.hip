@@ -74,14 +74,16 @@ __device__ __forceinline__ double swap_pair(double x) {
   return __hiloint2double(hi2, lo2);
 }
 __device__ __forceinline__ int swap_pair_i(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }
+// x (>= +0 or NaN) with its sign bit set to bit
+__device__ __forceinline__ double with_sign(double x, int bit) {
+  return __hiloint2double((__double2hiint(x) & 0x7FFFFFFF) | (bit << 31), __double2loint(x));
+}
 
 template <int T, int RV, int RC, int DV, int DC, bool SYN, bool FAST>
 __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, int cw, unsigned char *smem,
                                            unsigned hd, const unsigned (&vaddr)[RV][DV], const double (&pv)[RV],
                                            const int (&crow)[RC], const unsigned (&rb)[RC], const unsigned (&rb2)[RC],
-                                           const unsigned (&wb)[RC],
-                                           const unsigned (&ccol)[RC][(DC + 1) / 2], int odd, int &iter_out,
-                                           bool &conv_out) {
+                                           const unsigned (&wb)[RC], int odd, int &iter_out, bool &conv_out) {
   static_assert(DC % 2 == 0, "the lane-pair split assumes an even row degree");
   constexpr int H = DC / 2;
   int iter = 0;
@@ -106,6 +108,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
 #pragma unroll
         for (int k = 0; k < DV; ++k) c0s[r][k] = iter == 0 ? 0.5 : lds_ld<double>(vaddr[r][k]);
       double a0[RV], a1[RV], al0[RV][DV], al1[RV][DV];
+      int hb[RV];
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
         a0[r] = pv[r];
@@ -122,8 +125,10 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
           const double n1 = a1[r] * (1.0 - c0);
           if (k + 1 < DV)
             div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r]);
-          else  // the posterior only feeds the hard decision
-            lds_st<unsigned char>(hd + r * T, (unsigned char)hard_decision<FAST>(n0, n1));
+          else {  // the posterior only feeds the hard decision
+            hb[r] = hard_decision<FAST>(n0, n1);
+            lds_st<unsigned char>(hd + r * T, (unsigned char)hb[r]);
+          }
         }
       double b0[RV], b1[RV];
 #pragma unroll
@@ -143,7 +148,9 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
             div2<FAST, true>(t0, t1, t0 + t1, q0, q1);
           else
             div2<FAST>(t0, t1, t0 + t1, q0, q1);
-          lds_st<dbl2>(vaddr[r][k] & ~15u, dbl2{q0, q1});
+          // the column's decision rides in the sign bit of q1 (a probability,
+          // >= +0): the CN chains that load the message collect the parity
+          lds_st<dbl2>(vaddr[r][k] & ~15u, dbl2{q0, with_sign(q1, hb[r])});
           if (k > 0) {
             const double c0 = c0s[r][k];
             if (unit) {  // (c0, 1 - c0) / (c0 + (1 - c0)): the sum rounds to exactly 1 (bp_common.hpp)
@@ -158,19 +165,14 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
     }
     __syncthreads();
 
-    // ------------------------------------------------ early-stop parity check
-    int fail = 0;
-#pragma unroll
-    for (int r = 0; r < RC; ++r) {
-      int p = 0;
-#pragma unroll
-      for (int k = 0; k < H; ++k) p ^= lds_ld<unsigned char>(ccol[r][k]);
-      fail |= p ^ swap_pair_i(p);
-    }
-    // The OR over the workgroup is folded into the CN phase's closing barrier:
-    // the CN phase runs speculatively, and a converged codeword (no failing
-    // row) discards it — its slots are never read again and its syndromes are
-    // only written when the phase counts.
+    // The early-stop parity check rides on the CN phase: in steps 0..H-1 the
+    // even lane loads the row's edges [0, H) and the odd lane [H, DC), whose
+    // q1 words carry the columns' decisions in their sign bits.  The OR over
+    // the workgroup is folded into the CN phase's closing barrier: the CN
+    // phase runs speculatively, and a converged codeword (no failing row)
+    // discards it — its slots are never read again and its syndromes are only
+    // written when the phase counts.
+    unsigned par[RC];
 
     // ------------------------------------------------------------ CN phase
     double syn0[RC];
@@ -187,6 +189,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
       for (int r = 0; r < RC; ++r) {
         s0[r] = 1.0;
         s1[r] = 0.0;
+        par[r] = 0;
       }
       __builtin_amdgcn_s_setprio(2);
 #pragma unroll
@@ -201,8 +204,9 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
             // edge (odd ? DC-1-st : st): physical slot 2st+odd of the row while
             // st < H, 2(DC-1-st)+1-odd after (layout.cpp)
             const dbl2 m = st < H ? lds_ld<dbl2>(rb[r] + st * 32) : lds_ld<dbl2>(rb2[r] + (DC - 1 - st) * 32);
+            if (st < H) par[r] ^= (unsigned)__double2hiint(m.y);
             m0[r] = m.x;
-            m1[r] = m.y;
+            m1[r] = fabs(m.y);  // clear the decision bit
           }
         }
         if (st < H) {
@@ -240,6 +244,12 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
       }
 #pragma unroll
       for (int r = 0; r < RC; ++r) syn0[r] = s0[r];
+    }
+    int fail = 0;
+#pragma unroll
+    for (int r = 0; r < RC; ++r) {
+      const int p = (int)(par[r] >> 31);
+      fail |= p ^ swap_pair_i(p);
     }
     if (!__syncthreads_or(fail)) {  // every row satisfied before this CN phase
       conv = true;
@@ -292,7 +302,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
   }
   const int chalf = ((tid >> 3) & 1) * 8;  // bit 2 of the CN position (tid >> 1)
   int crow[RC], cbase[RC];
-  unsigned rb[RC], rb2[RC], wb[RC], ccol[RC][H];
+  unsigned rb[RC], rb2[RC], wb[RC];
 #pragma unroll
   for (int r = 0; r < RC; ++r) {
     const int row = c.cn_order[r * (T / 2) + (tid >> 1)];
@@ -303,12 +313,6 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
     rb2[r] = rb[r] + 16 - 32 * odd;
     wb[r] = rb[r] + chalf;
     asm volatile("" : "+v"(rb[r]), "+v"(rb2[r]), "+v"(wb[r]));
-#pragma unroll
-    for (int k = 0; k < H; ++k) {  // parity columns: even lane edges [0, DC/2), odd lane [DC/2, DC)
-      const int e = odd ? DC / 2 + k : k;
-      ccol[r][k] = cch_a + (unsigned)c.reg_pos[c.row_col[cbase[r] + (e < DC ? e : DC - 1)]];
-      asm volatile("" : "+v"(ccol[r][k]));  // keep the absolute address (no base re-add per use)
-    }
   }
 
 #if KML_STAMPS
@@ -359,10 +363,9 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
     int iter = 0;
     bool conv = false;
     if (fast)
-      decode_reg<T, RV, RC, DV, DC, SYN, true>(c, a, cw, smem, cch_a + tid, vaddr, pv, crow, rb, rb2, wb, ccol, odd, iter,
-                                              conv);
+      decode_reg<T, RV, RC, DV, DC, SYN, true>(c, a, cw, smem, cch_a + tid, vaddr, pv, crow, rb, rb2, wb, odd, iter, conv);
     else
-      decode_reg<T, RV, RC, DV, DC, SYN, false>(c, a, cw, smem, cch_a + tid, vaddr, pv, crow, rb, rb2, wb, ccol, odd, iter,
+      decode_reg<T, RV, RC, DV, DC, SYN, false>(c, a, cw, smem, cch_a + tid, vaddr, pv, crow, rb, rb2, wb, odd, iter,
                                                conv);
 
     REG_STAMP(3);
@@ -385,9 +388,12 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
         int cnt = 0;
 #pragma unroll
         for (int r = 0; r < RC; ++r) {
-          int p = 0;
+          int p = 0;  // ParityCheck of the final decisions (once per codeword: the columns from global)
 #pragma unroll
-          for (int k = 0; k < H; ++k) p ^= lds_ld<unsigned char>(ccol[r][k]);
+          for (int k = 0; k < H; ++k) {
+            const int e = odd ? DC / 2 + k : k;
+            p ^= cch[c.reg_pos[c.row_col[cbase[r] + (e < DC ? e : DC - 1)]]];
+          }
           const int full = p ^ swap_pair_i(p);
           if (!odd) cnt += full;
         }
