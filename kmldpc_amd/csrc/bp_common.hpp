@@ -25,6 +25,28 @@ __device__ __forceinline__ void lds_st(unsigned a, T v) {
   *(__attribute__((address_space(3))) T *)(size_t)a = v;
 }
 
+// Workgroup OR of a predicate with one barrier: each wave's lane 0 stores the
+// wave's ballot to its own LDS word, and after the barrier every lane ORs the
+// NW words (vector loads).  (__syncthreads_or goes through a two-barrier
+// library reduction: ~650 more cycles per call at 12 waves.)  The words need
+// no reset: a wave rewrites its word only after a later barrier that every
+// reader of the previous values has passed — callers must place one between
+// two calls (the BP kernels' VN-phase barrier).
+template <int NW>
+__device__ __forceinline__ int wg_any(int pred, int *wflags) {
+  static_assert(NW % 4 == 0 && NW <= 16, "wave flags are read as int4");
+  const int any = __ballot(pred) != 0;
+  if ((threadIdx.x & 63) == 0) wflags[threadIdx.x >> 6] = any;
+  __syncthreads();
+  int r = 0;
+#pragma unroll
+  for (int w = 0; w < NW; w += 4) {
+    const int4 v = *reinterpret_cast<const int4 *>(wflags + w);
+    r |= v.x | v.y | v.z | v.w;
+  }
+  return r;
+}
+
 // q0 = n0 / s and q1 = n1 / s, both correctly rounded.
 //
 // FAST = false: two IEEE divisions.

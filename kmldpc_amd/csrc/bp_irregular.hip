@@ -284,6 +284,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
   auto pbase = [](unsigned w) { return (int)(w & 0x3FFFu); };
   auto pdeg = [](unsigned w) { return (int)((w >> 14) & 15u); };
   auto pitem = [](unsigned w) { return (int)(w >> 18); };
+  __shared__ __attribute__((aligned(16))) int wflags[16];  // wg_any (bp_common.hpp)
   int iter = 0;
   bool conv = false;
   auto prior = [&](int v) { return v >= c.punct ? p0s[v - c.punct] : 0.5; };  // :126-134
@@ -359,7 +360,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
       if (cp[r] != ~0u) fail |= full;
     }
     IRR_STAMP(5);
-    if (!__syncthreads_or(fail)) {
+    if (!wg_any<T / 64>(fail, wflags)) {
       conv = true;
       break;
     }

@@ -52,6 +52,17 @@ constexpr int kRedBytes = 16;
 #endif
 #if KML_STAMPS
 __device__ unsigned long long kml_reg_stamps[8];
+// per wave (lane 0), summed over codewords: [0] VN compute, [1] VN barrier
+// wait, [2] CN compute, [3] CN barrier wait (+ OR)
+__device__ unsigned long long kml_reg_wave_stamps[16][4];
+#define REG_WSTAMP(i)                                              \
+  do {                                                             \
+    if ((threadIdx.x & 63) == 0) {                                 \
+      const unsigned long long _t = __builtin_amdgcn_s_memtime();  \
+      ws_acc[(i)] += _t - ws_prev;                                 \
+      ws_prev = _t;                                                \
+    }                                                              \
+  } while (0)
 #define REG_STAMP(i)                                               \
   do {                                                             \
     if (tid == 0) {                                                \
@@ -63,6 +74,9 @@ __device__ unsigned long long kml_reg_stamps[8];
 #else
 #define REG_STAMP(i) \
   do {               \
+  } while (0)
+#define REG_WSTAMP(i) \
+  do {                \
   } while (0)
 #endif
 
@@ -86,8 +100,12 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
                                            const unsigned (&wb)[RC], int odd, int &iter_out, bool &conv_out) {
   static_assert(DC % 2 == 0, "the lane-pair split assumes an even row degree");
   constexpr int H = DC / 2;
+  __shared__ __attribute__((aligned(16))) int wflags[16];  // wg_any (bp_common.hpp)
   int iter = 0;
   bool conv = false;
+#if KML_STAMPS
+  unsigned long long ws_acc[4] = {0, 0, 0, 0}, ws_prev = __builtin_amdgcn_s_memtime();
+#endif
   for (; iter < a.iter_count; ++iter) {
     // Wave priorities (s_setprio) fall as a wave advances through a phase, so
     // the SIMD arbiter (priority, then age) favours the waves that are behind:
@@ -163,7 +181,9 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
         }
       }
     }
+    REG_WSTAMP(0);
     __syncthreads();
+    REG_WSTAMP(1);
 
     // The early-stop parity check rides on the CN phase: in steps 0..H-1 the
     // even lane loads the row's edges [0, H) and the odd lane [H, DC), whose
@@ -251,7 +271,10 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
       const int p = (int)(par[r] >> 31);
       fail |= p ^ swap_pair_i(p);
     }
-    if (!__syncthreads_or(fail)) {  // every row satisfied before this CN phase
+    REG_WSTAMP(2);
+    const int any_fail = wg_any<T / 64>(fail, wflags);
+    REG_WSTAMP(3);
+    if (!any_fail) {  // every row satisfied before this CN phase
       conv = true;
       break;
     }
@@ -261,6 +284,10 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
         if (!odd) a.syn[(long long)cw * c.M + crow[r]] = syn0[r];  // alpha past the last edge (:274)
     }
   }
+#if KML_STAMPS
+  if ((threadIdx.x & 63) == 0)
+    for (int i = 0; i < 4; ++i) atomicAdd(&kml_reg_wave_stamps[threadIdx.x >> 6][i], ws_acc[i]);
+#endif
   iter_out = iter;
   conv_out = conv;
 }
@@ -477,9 +504,12 @@ hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s)
 }  // namespace kml
 extern "C" int kml_debug_reg_stamps(unsigned long long *out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(kml::kml_reg_stamps), sizeof(kml::kml_reg_stamps));
+  if (e == hipSuccess)  // then the per-wave phase sums (16 x 4)
+    e = hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(kml::kml_reg_wave_stamps), sizeof(kml::kml_reg_wave_stamps));
   if (reset) {
-    unsigned long long zero[8] = {};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(kml::kml_reg_stamps), zero, sizeof(zero));
+    unsigned long long zero[8 + 64] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(kml::kml_reg_stamps), zero, sizeof(kml::kml_reg_stamps));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(kml::kml_reg_wave_stamps), zero, sizeof(kml::kml_reg_wave_stamps));
   }
   return e == hipSuccess ? 0 : -3;
 }

@@ -34,18 +34,22 @@ def main():
     ctx.sim_generate(2.0, B, seed=3)
     fn = K.lib().kml_debug_reg_stamps
     fn.argtypes = [C.c_void_p, C.c_int]
-    buf = np.zeros(8, np.uint64)
+    buf = np.zeros(8 + 64, np.uint64)
     ctx.sim_decode(2.0)  # warm-up
     fn(buf.ctypes.data, 1)
     ctx.sim_decode(2.0)
     fn(buf.ctypes.data, 0)
-    st = buf.astype(np.float64)
+    st = buf[:8].astype(np.float64)
+    ws = buf[8:].reshape(16, 4).astype(np.float64)
     ncw, its = st[6], st[7]
     print(f"bp_regular_kernel: {int(ncw)} codewords, {its / ncw:.2f} CN phases per codeword")
     tot = st[:6].sum() / ncw
     for i, n in enumerate(NAMES):
         print(f"  {n:24s} {st[i] / ncw:9.0f} cycles/cw  {100 * st[i] / ncw / tot:5.1f}%")
     print(f"  {'total':24s} {tot:9.0f} cycles/cw; iterations {st[3] / max(its, 1):.0f} cycles per CN phase")
+    print("  per wave, cycles per CN phase: VN compute, VN barrier, CN compute, CN barrier")
+    for w in range(12):
+        print(f"    wave {w:2d}: " + " ".join(f"{x / max(its, 1):7.0f}" for x in ws[w]))
 
 
 if __name__ == "__main__":
