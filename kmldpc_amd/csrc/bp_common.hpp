@@ -47,6 +47,11 @@ __device__ __forceinline__ int wg_any(int pred, int *wflags) {
   return r;
 }
 
+template <int NW>
+__device__ __forceinline__ int wg_all(int pred, int *wflags) {
+  return !wg_any<NW>(!pred, wflags);
+}
+
 // q0 = n0 / s and q1 = n1 / s, both correctly rounded.
 //
 // FAST = false: two IEEE divisions.

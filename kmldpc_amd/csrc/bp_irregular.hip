@@ -384,6 +384,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
 template <int T, bool SYN>
 __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, unsigned int *queue, int fast_allowed) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ __attribute__((aligned(16))) int pflags[16];  // wg_all of the FAST prior check (bp_common.hpp)
   const int tid = threadIdx.x;
   const int odd = tid & 1;
   double2 *slots = reinterpret_cast<double2 *>(smem);
@@ -422,7 +423,7 @@ __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, 
       ok = ok && fast_prior_ok(q);
     }
     for (int e = tid; e < c.irr_slots; e += T) slots[e].x = 0.5;  // InitMsg
-    const bool fast = __syncthreads_and(ok ? 1 : 0) && fast_allowed;
+    const bool fast = wg_all<T / 64>(ok ? 1 : 0, pflags) && fast_allowed;
 
     int iter = 0;
     bool conv = false;

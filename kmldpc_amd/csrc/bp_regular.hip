@@ -299,6 +299,7 @@ constexpr size_t p0s_offset(int E, int N) { return ((size_t)E * 16 + kRedBytes +
 template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB>
 __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, unsigned int *queue, int fast_allowed) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ __attribute__((aligned(16))) int pflags[16];  // wg_all of the FAST prior check (bp_common.hpp)
   // fused demap: the constellation and the exp table in LDS (demap_common.hpp)
   __shared__ double dcons[DMB > 0 ? (2 << DMB) : 2];
   __shared__ uint64_t detab[DMB > 0 ? 256 : 1];
@@ -384,7 +385,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
       pv[r] = (vcol[r] >= c.punct) ? p0[vcol[r] - c.punct] : 0.5;
       ok = ok && fast_prior_ok(pv[r]);
     }
-    const bool fast = __syncthreads_and(ok ? 1 : 0) && fast_allowed;
+    const bool fast = wg_all<T / 64>(ok ? 1 : 0, pflags) && fast_allowed;
     REG_STAMP(2);
 
     int iter = 0;
