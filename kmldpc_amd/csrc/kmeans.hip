@@ -827,19 +827,20 @@ __global__ __launch_bounds__(kFusedT) void km_fused_kernel(const double *__restr
       const bool own = lane < nq;
       const uint64_t oldb = own ? wbits[wl] : 0ull;
       uint64_t need = __ballot(own && (!incremental || !(drift < (double)wthr[wl])));
-      while (need) {  // wave-uniform
-        const int q = __builtin_ctzll(need);
-        need &= need - 1;
-        const int w = wave + NW * q;
-        const int j = w * 64 + lane;
-        bool m = false;
-        float t = INFINITY;
+      // two flagged words per pass: their LDS loads, distance screens and
+      // wave minima are independent chains that overlap
+      auto word = [&](int q, bool &m, float &t) {
+        const int j = (wave + NW * q) * 64 + lane;
+        m = false;
+        t = INFINITY;
         if (j < S) {
           double g;
           m = member0_margin<KC>(cl, ys[j].x, ys[j].y, g);
           t = (float)((drift + g * inv2c) * (1.0 - 0x1p-20));  // D + g / (2 Cmax), rounded down
         }
-        t = wave_min_f(t);
+      };
+      auto commit = [&](int q, bool m, float t) {
+        const int w = wave + NW * q;
         const uint64_t bits = __ballot(m);
         const uint64_t was = ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(oldb >> 32), q) << 32) |
                              (unsigned)__builtin_amdgcn_readlane((int)oldb, q);
@@ -848,8 +849,29 @@ __global__ __launch_bounds__(kFusedT) void km_fused_kernel(const double *__restr
           wbits[w] = bits;
           wthr[w] = t;
         }
+      };
+      while (need) {  // wave-uniform
+        const int q1 = __builtin_ctzll(need);
+        need &= need - 1;
+        if (need) {
+          const int q2 = __builtin_ctzll(need);
+          need &= need - 1;
+          bool m1, m2;
+          float t1, t2;
+          word(q1, m1, t1);
+          word(q2, m2, t2);
+          t1 = wave_min_f(t1);
+          t2 = wave_min_f(t2);
+          commit(q1, m1, t1);
+          commit(q2, m2, t2);
+        } else {
+          bool m1;
+          float t1;
+          word(q1, m1, t1);
+          commit(q1, m1, wave_min_f(t1));
+        }
 #if KML_STAMPS
-        if (tid == 0) km_acc[KS_WORDS] += 1;  // wave 0's words; x NW at the flush (an estimate)
+        if (tid == 0) km_acc[KS_WORDS] += 1;  // wave 0's passes; x NW at the flush (an estimate)
 #endif
       }
     }
