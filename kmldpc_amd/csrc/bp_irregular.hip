@@ -176,7 +176,20 @@ __device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], 
   for (int r = 0; r < R; ++r) sv[r] = s0[r];
 }
 
-// falling wave priorities over a phase's rounds (see bp_regular.hip)
+// falling wave priorities over a phase's rounds (see bp_regular.hip);
+// the levels are overridable for A/B builds
+#ifndef KML_IRR_PRIO_VN_PAIR
+#define KML_IRR_PRIO_VN_PAIR 3
+#endif
+#ifndef KML_IRR_PRIO_VN_SINGLE
+#define KML_IRR_PRIO_VN_SINGLE 1
+#endif
+#ifndef KML_IRR_PRIO_CN_PAIR
+#define KML_IRR_PRIO_CN_PAIR 2
+#endif
+#ifndef KML_IRR_PRIO_CN_SINGLE
+#define KML_IRR_PRIO_CN_SINGLE 0
+#endif
 __device__ __forceinline__ void set_prio(int p) {
   switch (p) {
     case 3: __builtin_amdgcn_s_setprio(3); break;
@@ -302,7 +315,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
       asm volatile("" : "+v"(vp[r]), "+v"(cp[r]));
     }
     asm volatile("" : "+v"(od));
-    set_prio(3);
+    set_prio(KML_IRR_PRIO_VN_PAIR);
     if (vp[0] != ~0u) {  // paired round: two columns of one degree, interleaved
       const int v0 = pitem(vp[0]), v1 = pitem(vp[1]);
       const unsigned short *const cs[2] = {cslot + pbase(vp[0]), cslot + pbase(vp[1])};
@@ -311,7 +324,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
       vn_any<2, FAST>(pdeg(vp[0]), slots, cs, p, h);
     }
     IRR_STAMP(0);
-    set_prio(1);
+    set_prio(KML_IRR_PRIO_VN_SINGLE);
     if (vp[2] != ~0u) {
       const int v = pitem(vp[2]);
       const unsigned short *const cs[1] = {cslot + pbase(vp[2])};
@@ -331,7 +344,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
     double sv[3] = {0.0, 0.0, 0.0};
     unsigned par[3] = {0u, 0u, 0u};
     IRR_STAMP(3);
-    set_prio(2);
+    set_prio(KML_IRR_PRIO_CN_PAIR);
     if (cp[0] != ~0u) {  // both lanes of a pair agree
       const int base[2] = {pbase(cp[0]), pbase(cp[1])};
       double s2[2];
@@ -343,7 +356,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
       par[1] = p2[1];
     }
     IRR_STAMP(4);
-    set_prio(0);
+    set_prio(KML_IRR_PRIO_CN_SINGLE);
     if (cp[2] != ~0u) {
       const int base[1] = {pbase(cp[2])};
       double s1[1];
