@@ -295,6 +295,12 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
 // Dynamic LDS: E slots of 16 B, the reduction words, N hard-decision bytes,
 // then (fused demap only, 16-byte aligned) the codeword's N priors.
 constexpr size_t p0s_offset(int E, int N) { return ((size_t)E * 16 + kRedBytes + (size_t)N + 15) & ~(size_t)15; }
+// then the info bits' positions in the decision bytes (u16, K entries), staged
+// once per workgroup for the epilogue's CntErr
+constexpr size_t ipos_offset(int E, int N, int DMB) {
+  return DMB > 0 ? p0s_offset(E, N) + (size_t)N * 8 : (((size_t)E * 16 + kRedBytes + (size_t)N + 1) & ~(size_t)1);
+}
+constexpr size_t reg_lds_bytes(int E, int N, int K, int DMB) { return ipos_offset(E, N, DMB) + (size_t)K * 2; }
 
 template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB>
 __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, unsigned int *queue, int fast_allowed) {
@@ -315,6 +321,8 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
   unsigned char *cch = smem + (size_t)c.E * 16 + kRedBytes;
 
   const unsigned smem_a = lds_addr(smem), cch_a = lds_addr(cch);
+  unsigned short *ipos = reinterpret_cast<unsigned short *>(smem + ipos_offset(c.E, c.N, DMB));
+  for (int i = tid; i < c.K; i += T) ipos[i] = (unsigned short)c.reg_pos[c.info_off + i];
   int vcol[RV];
   unsigned vaddr[RV][DV];
 #pragma unroll
@@ -427,10 +435,20 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
         }
         if (cnt) atomicAdd(&red[0], cnt);
       }
-      if (a.ref_bits) {
-        const int errs =
-            count_info_errors<T>(cch, c.reg_pos, c.info_off, c.K, c.Kw, a.ref_bits + (long long)cw * c.Kw, tid);
-        if (errs) atomicAdd(&red[1], errs);
+      if (a.ref_bits) {  // CntErr (sourcesink.cc:29-47): two 64-bit words per wave and round, loads first
+        const uint64_t *ref = a.ref_bits + (long long)cw * c.Kw;
+        const int lane = tid & 63;
+        int errs = 0;
+        for (int w0 = tid >> 6; w0 < c.Kw; w0 += 2 * (T / 64)) {
+          const int w1 = w0 + T / 64;
+          const uint64_t r0 = ref[w0], r1 = w1 < c.Kw ? ref[w1] : 0ull;
+          const int i0 = w0 * 64 + lane, i1 = w1 * 64 + lane;
+          const int b0 = i0 < c.K ? cch[ipos[i0]] : 0;
+          const int b1 = i1 < c.K && w1 < c.Kw ? cch[ipos[i1]] : 0;
+          const uint64_t m0 = __ballot(b0), m1 = __ballot(b1);
+          errs += __popcll(m0 ^ r0) + (w1 < c.Kw ? __popcll(m1 ^ r1) : 0);
+        }
+        if (lane == 0 && errs) atomicAdd(&red[1], errs);
       }
     }
     __syncthreads();
@@ -465,7 +483,8 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
 template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB>
 hipError_t launch_reg_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
   auto kern = bp_regular_kernel<T, RV, RC, DV, DC, SYN, DMB>;
-  const size_t lds = DMB > 0 ? p0s_offset(c.E, c.N) + (size_t)c.N * 8 : (size_t)c.E * 16 + kRedBytes + (size_t)c.N;
+  const size_t lds = reg_lds_bytes(c.E, c.N, c.K, DMB);
+  if (lds > 160 * 1024 || c.K > 65536 || c.N > 65536) return hipErrorNotSupported;
   hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   int dev = 0, ncu = 0;
@@ -521,7 +540,7 @@ bool bp_regular_fuses_demap(const DevCode &c, int bits) {
   if (const char *e = getenv("KML_FUSED_DEMAP"))
     if (e[0] == '0') return false;
   return c.reg_c2v && bp_regular_threads(c.N, c.M, c.E, c.dv_max, c.dc_max, c.regular) == 768 && c.punct == 0 &&
-         bits == 2 && c.cc_len % bits == 0 && p0s_offset(c.E, c.N) + (size_t)c.N * 8 <= 160 * 1024;
+         bits == 2 && c.cc_len % bits == 0 && reg_lds_bytes(c.E, c.N, c.K, 2) <= 160 * 1024;
 }
 
 }  // namespace kml
