@@ -50,6 +50,16 @@ constexpr int kRedBytes = 16;
 #ifndef KML_STAMPS
 #define KML_STAMPS 0
 #endif
+// CN-phase wave priorities: s > 0 ranks the waves by age (the youngest third
+// highest) until step s, then all at 0 — the oldest waves otherwise win the
+// arbiter's age tie-break and finish 1.2K cycles before the youngest (per-wave
+// stamps); measured 5 (-0.7..0.9%) against falling-by-step (0), 2, 3 and 6.
+#ifndef KML_CN_AGE_PRIO
+#define KML_CN_AGE_PRIO 5
+#endif
+#ifndef KML_VN_AGE_PRIO  // (A/B) 1: VN priorities by wave age for the whole phase (measured +4%: off)
+#define KML_VN_AGE_PRIO 0
+#endif
 #if KML_STAMPS
 __device__ unsigned long long kml_reg_stamps[8];
 // per wave (lane 0), summed over codewords: [0] VN compute, [1] VN barrier
@@ -112,7 +122,16 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
     // the 3 waves of a SIMD reach the barrier together instead of the oldest
     // finishing first and the youngest running its dependent chains alone.
     // Measured: per-phase end-time spread 3100 -> 500 cycles, kernel -2.5%.
+#if KML_VN_AGE_PRIO
+    {
+      const int grp = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / 4;  // 0 oldest .. 2 youngest
+      if (grp >= 2) __builtin_amdgcn_s_setprio(3);
+      else if (grp == 1) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(1);
+    }
+#else
     __builtin_amdgcn_s_setprio(3);
+#endif
     // The RV columns' chains are interleaved step by step in program order so
     // their dependent fma / rcp sequences overlap.  On the FAST path the
     // boundary state beta = (1, 1) is applied as the identity (x * 1.0 == x).
@@ -151,11 +170,15 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
       double b0[RV], b1[RV];
 #pragma unroll
       for (int r = 0; r < RV; ++r) b0[r] = b1[r] = 1.0;
+#if !KML_VN_AGE_PRIO
       __builtin_amdgcn_s_setprio(2);
+#endif
 #pragma unroll
       for (int k = DV - 1; k >= 0; --k) {
+#if !KML_VN_AGE_PRIO
         if (k == DV - 2) __builtin_amdgcn_s_setprio(1);
         if (k == DV - 3) __builtin_amdgcn_s_setprio(0);
+#endif
 #pragma unroll
         for (int r = 0; r < RV; ++r) {
           const bool unit = FAST && k == DV - 1;  // beta = (1, 1)
@@ -211,11 +234,24 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
         s1[r] = 0.0;
         par[r] = 0;
       }
+#if KML_CN_AGE_PRIO  // (A/B) the youngest waves start the CN phase at the highest priority
+      {
+        const int grp = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / 4;  // 0 oldest .. 2 youngest
+        if (grp >= 2) __builtin_amdgcn_s_setprio(3);
+        else if (grp == 1) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(1);
+      }
+#else
       __builtin_amdgcn_s_setprio(2);
+#endif
 #pragma unroll
       for (int st = 0; st < DC; ++st) {
+#if KML_CN_AGE_PRIO
+        if (st == KML_CN_AGE_PRIO) __builtin_amdgcn_s_setprio(0);
+#else
         if (st == 2) __builtin_amdgcn_s_setprio(1);
         if (st == 4) __builtin_amdgcn_s_setprio(0);
+#endif
         const bool advance = SYN || st + 1 < DC;
         double m0[RC], m1[RC];
         if (advance) {
