@@ -187,6 +187,9 @@ __device__ __forceinline__ void cn_halves(double2 *slots, const int (&base)[R], 
 #ifndef KML_IRR_PRIO_CN_PAIR
 #define KML_IRR_PRIO_CN_PAIR 2
 #endif
+#ifndef KML_IRR_CN_AGE_PRIO
+#define KML_IRR_CN_AGE_PRIO 0
+#endif
 #ifndef KML_IRR_PRIO_CN_SINGLE
 #define KML_IRR_PRIO_CN_SINGLE 0
 #endif
@@ -344,7 +347,11 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
     double sv[3] = {0.0, 0.0, 0.0};
     unsigned par[3] = {0u, 0u, 0u};
     IRR_STAMP(3);
+#if KML_IRR_CN_AGE_PRIO  // (A/B) the CN pair round's priority by wave age (youngest third highest)
+    set_prio(1 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * 3 / (T / 64));
+#else
     set_prio(KML_IRR_PRIO_CN_PAIR);
+#endif
     if (cp[0] != ~0u) {  // both lanes of a pair agree
       const int base[2] = {pbase(cp[0]), pbase(cp[1])};
       double s2[2];
