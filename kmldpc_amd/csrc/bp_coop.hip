@@ -820,6 +820,9 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
 #ifndef KML_PART_CN_AGE_PRIO
 #define KML_PART_CN_AGE_PRIO 5
 #endif
+#ifndef KML_PART_VN_AGE_PRIO
+#define KML_PART_VN_AGE_PRIO 0
+#endif
 constexpr unsigned kTagHi = 0x80000000u;  // bit 63 of a message word (hi dword bit 31)
 constexpr unsigned kHdHi = 0x40000000u;   // bit 62: hard decision (v2c first word)
 
@@ -928,7 +931,17 @@ __device__ __forceinline__ bool part_iterations_tagged(
     // (c2v of cut edges sit in the mirror slots, received at the end of the
     // previous iteration; iteration 0 reads InitMsg's 0.5)
     if (run) {
+#if KML_PART_VN_AGE_PRIO  // (A/B) VN priorities by wave age for the whole phase (measured +5%: off)
+      {
+        const int grp = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * 4 / NW;
+        if (grp >= 3) __builtin_amdgcn_s_setprio(3);
+        else if (grp == 2) __builtin_amdgcn_s_setprio(2);
+        else if (grp == 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+#else
       __builtin_amdgcn_s_setprio(3);
+#endif
       double c0s[RV][DV];
 #pragma unroll
       for (int r = 0; r < RV; ++r)
@@ -962,11 +975,15 @@ __device__ __forceinline__ bool part_iterations_tagged(
       double b0[RV], b1[RV];
 #pragma unroll
       for (int r = 0; r < RV; ++r) b0[r] = b1[r] = 1.0;
+#if !KML_PART_VN_AGE_PRIO
       __builtin_amdgcn_s_setprio(2);
+#endif
 #pragma unroll
       for (int k = DV - 1; k >= 0; --k) {
+#if !KML_PART_VN_AGE_PRIO
         if (k == DV - 2) __builtin_amdgcn_s_setprio(1);
         if (k == DV - 3) __builtin_amdgcn_s_setprio(0);
+#endif
 #pragma unroll
         for (int r = 0; r < RV; ++r) {
           const bool unit = k == DV - 1;
