@@ -927,6 +927,12 @@ __device__ __forceinline__ bool part_iterations_tagged(
     const bool run = iter < a.iter_count;  // else only the last CN phase's early-stop check remains
     uint8_t *decb = dec + (iter & 1) * NG;
     KML_STAMP(0);
+    // wave 0 issues the load of the members' early-stop flags of iteration
+    // g - 1 now: it is used after this VN phase and the v2c receive, so its L2
+    // round trip overlaps them (the flags were posted before the partners'
+    // c2v messages this member received)
+    unsigned long long vflag = 0;
+    if (iter > 0 && tid < kG) vflag = ld_rlx64(&gs->mflag[(g - 1) & 1][tid]);
     // ------------------------------------------------------------ VN phase
     // (c2v of cut edges sit in the mirror slots, received at the end of the
     // previous iteration; iteration 0 reads InitMsg's 0.5)
@@ -1024,7 +1030,7 @@ __device__ __forceinline__ bool part_iterations_tagged(
       unsigned long long v = (unsigned long long)g << 1;
       if (tid < kG) {
         for (long long spin = 0;; ++spin) {
-          v = ld_rlx64(&gs->mflag[(g - 1) & 1][tid]);
+          v = spin == 0 ? vflag : ld_rlx64(&gs->mflag[(g - 1) & 1][tid]);  // first: the load issued before VN
           if ((v >> 1) == (unsigned long long)g) break;
           if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
             __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
