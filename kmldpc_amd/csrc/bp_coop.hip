@@ -68,6 +68,9 @@ size_t part_lds_bytes(const DevCode &c) {
   return ((size_t)c.M / kPartG * 6 + (size_t)c.pt_mirror) * 16 + (size_t)c.N;
 }
 
+#ifndef KML_POLL_SLEEP  // (A/B) s_sleep between the tagged mailbox polls
+#define KML_POLL_SLEEP 0  // measured: no sleep 8.52 -> 8.48 ms per 4096 PEG8064 codewords
+#endif
 constexpr long long kSpinLimit = 20000000;  // ~1 s of s_sleep(1) polls
 
 // The tagged mailboxes (bp_part_kernel) follow the barrier-exchange ones in
@@ -897,7 +900,7 @@ __device__ __forceinline__ bool poll_entries(const int (&ent)[R], __amdgpu_buffe
       __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
-    __builtin_amdgcn_s_sleep(1);
+    if (KML_POLL_SLEEP) __builtin_amdgcn_s_sleep(1);
   }
 }
 
