@@ -875,8 +875,15 @@ __device__ __forceinline__ bool poll_entries(const int (&ent)[R], __amdgpu_buffe
 #pragma unroll
     for (int q = 0; q < R; ++q)
       if (need[q]) {
+        if constexpr (W == 2) {  // one 16-byte load (each word carries its own tag)
+          const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(mb, (int)(mb_off + (unsigned)(ent[q] >> 16) * 16u), 0,
+                                                                kAuxSc1);
+          w[q][0] = ((unsigned long long)v.y << 32) | v.x;
+          w[q][1] = ((unsigned long long)v.w << 32) | v.z;
+        } else {
 #pragma unroll
-        for (int i = 0; i < W; ++i) w[q][i] = mb_ld64(mb, mb_off + (unsigned)(ent[q] >> 16) * (8 * W) + 8 * i);
+          for (int i = 0; i < W; ++i) w[q][i] = mb_ld64(mb, mb_off + (unsigned)(ent[q] >> 16) * (8 * W) + 8 * i);
+        }
       }
     bool pend = false;
 #pragma unroll
