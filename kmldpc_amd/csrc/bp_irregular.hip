@@ -26,6 +26,12 @@
 //     swaps exchange the chain states, each lane finishes half of the row's
 //     c2v messages (for an odd degree the even lane also takes the middle
 //     edge, from the two states both lanes hold at that step);
+//   * the slots are laid out in per-wave blocks, a row's edges 32 slots apart
+//     (layout.hpp kIrrCnStride), so a CN step reads contiguous runs;
+//   * the VN phase leaves each column's decision in the sign bit of its v2c
+//     q1 words, and the CN chains XOR the ones they load: the early-stop
+//     parity costs no pass of its own, and its workgroup OR is one barrier
+//     (bp_common.hpp wg_any).  Measured: 19.5 ms (round-2 start) -> 14.7 ms;
 //   * the shared-reciprocal exact division (bp_common.hpp) on codewords whose
 //     priors qualify.
 #include "bp_common.hpp"
