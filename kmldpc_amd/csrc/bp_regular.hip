@@ -19,8 +19,13 @@
 //     both lanes evaluate the same formula on (own state, partner state) and
 //     the result is the reference's bit for bit.  2M == RC*T half-rows:
 //     the CN phase has exactly as many lanes busy as the VN phase.
-//   * the early-stop parity check XORs the two half-rows through the same DPP
-//     swap.
+//   * the early-stop parity check rides on the CN phase: the VN phase leaves
+//     each column's decision in the sign bit of its q1 words, each lane XORs
+//     the ones of its half-row as its chain loads them, and the pair combines
+//     the halves through the same DPP swap; the workgroup OR is one barrier
+//     (bp_common.hpp wg_any).
+//   * wave priorities: falling by step in the VN phase, by wave age in the CN
+//     phase (KML_CN_AGE_PRIO).
 //   * LDS placement (layout.hpp): the columns' lane assignment is annealed on
 //     the host against the VN phase's bank conflicts, the hard decisions are
 //     stored by lane position (contiguous byte stores), rows are stored in CN
