@@ -363,6 +363,10 @@ namespace kml {
 namespace {
 
 // One wave's worth of items (64 columns, or 32 rows) for one round.
+#ifndef KML_IRR_PARTIAL_PAIRS
+#define KML_IRR_PARTIAL_PAIRS 1
+#endif
+
 struct WaveItems {
   std::vector<int32_t> a, b;  // a: the (first) items; b: the second items of a pair wave
   double cost = 0;
@@ -383,6 +387,20 @@ bool plan_rounds(std::vector<std::vector<int32_t>> items, int per_wave, int W, i
       w.b.assign(items[d].begin() + per_wave, items[d].begin() + 2 * per_wave);
       items[d].erase(items[d].begin(), items[d].begin() + 2 * per_wave);
       w.cost = 2 * per_wave * cost(d);
+      pairs.push_back(std::move(w));
+    }
+  // leftover pair slots take a partial pair wave of one degree (at least half
+  // a wave of pairs, lowest degrees first), so that fewer single waves mix
+  // two degrees (a mixed wave runs both degrees' code paths)
+  if (KML_IRR_PARTIAL_PAIRS)
+    for (int d = 0; d <= std::min(dmax, pair_max) && (int)pairs.size() < W; ++d) {
+      const int np = (int)items[d].size() / 2;
+      if (np < per_wave / 2 || np >= per_wave) continue;
+      WaveItems w;
+      w.a.assign(items[d].begin(), items[d].begin() + np);
+      w.b.assign(items[d].begin() + np, items[d].begin() + 2 * np);
+      items[d].erase(items[d].begin(), items[d].begin() + 2 * np);
+      w.cost = 2 * np * cost(d);
       pairs.push_back(std::move(w));
     }
   // the rest as single waves, highest degree first; a partial wave is topped up
@@ -451,14 +469,14 @@ bool plan_irregular(const LdpcCode &L, int T, int vn_pair_max, int cn_pair_max, 
   out.cn.assign(3 * T / 2, -1);
   for (int w = 0; w < W; ++w) {
     if (vp_of[w] >= 0)
-      for (int l = 0; l < 64; ++l) {
+      for (size_t l = 0; l < vp[vp_of[w]].a.size(); ++l) {  // (a partial pair wave leaves lanes idle)
         out.vn[w * 64 + l] = vp[vp_of[w]].a[l];
         out.vn[T + w * 64 + l] = vp[vp_of[w]].b[l];
       }
     if (vs_of[w] >= 0)
       for (size_t l = 0; l < vs[vs_of[w]].a.size(); ++l) out.vn[2 * T + w * 64 + l] = vs[vs_of[w]].a[l];
     if (cp_of[w] >= 0)
-      for (int l = 0; l < 32; ++l) {
+      for (size_t l = 0; l < cp[cp_of[w]].a.size(); ++l) {
         out.cn[w * 32 + l] = cp[cp_of[w]].a[l];
         out.cn[T / 2 + w * 32 + l] = cp[cp_of[w]].b[l];
       }
