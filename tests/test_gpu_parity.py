@@ -560,6 +560,27 @@ def test_extreme_inputs_match_oracle(data_dir, matrix, modem, is5g, max_iter):
         assert np.array_equal(r["syn"][i], syn, equal_nan=True), i
 
 
+@pytest.mark.parametrize("matrix,modem,is5g,max_iter", CODES)
+def test_nan_and_inf_priors_match_oracle(data_dir, matrix, modem, is5g, max_iter):
+    """NaN and +-inf priors (the IEEE path): the messages then carry NaNs, whose
+    sign bits the decision-in-sign-bit parity (bp_regular / bp_irregular) must
+    not confuse with a column's decision; the outputs equal the oracle's."""
+    ctx = ctx_for(data_dir, matrix, modem, is5g, max_iter)
+    oc = oracle_for(data_dir, matrix, is5g, max_iter)
+    n = ctx.cc_len
+    rng = np.random.default_rng(9)
+    base = rng.uniform(0.05, 0.95, n)
+    cases = [np.where(rng.random(n) < 0.01, np.nan, base), np.where(rng.random(n) < 0.01, -np.nan, base),
+             np.where(rng.random(n) < 0.01, np.inf, base), np.where(rng.random(n) < 0.01, -np.inf, base)]
+    p0 = np.stack(cases)
+    r = ctx.bp_decode(p0, cc_hat=True, syn=np.zeros((len(cases), ctx.M)))
+    for i in range(len(cases)):
+        ret, uh, cch, syn = oc.bp_decode(p0[i])
+        assert r["ret"][i] == ret, i
+        assert np.array_equal(r["cc_hat"][i], cch), i
+        assert np.array_equal(r["syn"][i], syn, equal_nan=True), i
+
+
 # ---------------------------------------------------------------- soft metric
 from conftest import load_soft_case, soft_case_names  # noqa: E402
 
