@@ -205,6 +205,35 @@ def test_kernel_placement_plans(tmp_path, data_dir):
     assert "plan_errors=0" in out.stdout
 
 
+def test_host_code_under_sanitizers(tmp_path, data_dir):
+    """The host side of the library (planner, GF(2) elimination + encoder,
+    TOML reader, constellation loader, reference frame stream) built with
+    AddressSanitizer + UndefinedBehaviorSanitizer: the placement-plan checks on
+    the reference's H files, encoded codewords with a zero syndrome, and the
+    error paths on truncated / garbage H and constellation files and broken
+    TOML (tests/native/host_san_check.cpp).  Any sanitizer finding aborts."""
+    csrc = os.path.join(REPO, "kmldpc_amd", "csrc")
+    flags = ["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+             "-fno-omit-frame-pointer", "-I", csrc]
+    host = [os.path.join(csrc, f) for f in ("code.cpp", "layout.cpp", "config.cpp", "modem.cpp", "refstream.cpp")]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    hsc, planc = tmp_path / "hsc", tmp_path / "planc"
+    subprocess.run(flags + ["-o", str(hsc), os.path.join(REPO, "tests", "native", "host_san_check.cpp")] + host,
+                   check=True)
+    subprocess.run(flags + ["-o", str(planc), os.path.join(REPO, "tests", "native", "plan_check.cpp")] + host[:2],
+                   check=True)
+    scratch = tmp_path / "scratch"
+    scratch.mkdir()
+    out = subprocess.run([str(hsc), data_dir, str(scratch)], capture_output=True, text=True, env=env, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr[-4000:]
+    assert "san_errors=0" in out.stdout
+    out = subprocess.run([str(planc)] + [os.path.join(data_dir, f) for f in
+                                         ("PEG2304regular0.5.txt", "5GLDPCBG2a3_R12_K960.txt", "PEG8064regular0.5.txt")],
+                         capture_output=True, text=True, env=env, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr[-4000:]
+    assert "plan_errors=0" in out.stdout
+
+
 def test_cn_division_tail_exact_near_one():
     """The CN phases' division (near-one reciprocal RN(1/s), then the FAST
     tail) rounds n / s correctly on every significand where it could fail, for
