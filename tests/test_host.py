@@ -218,10 +218,11 @@ def test_host_code_under_sanitizers(tmp_path, data_dir):
     host = [os.path.join(csrc, f) for f in ("code.cpp", "layout.cpp", "config.cpp", "modem.cpp", "refstream.cpp")]
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
     hsc, planc = tmp_path / "hsc", tmp_path / "planc"
-    subprocess.run(flags + ["-o", str(hsc), os.path.join(REPO, "tests", "native", "host_san_check.cpp")] + host,
-                   check=True)
-    subprocess.run(flags + ["-o", str(planc), os.path.join(REPO, "tests", "native", "plan_check.cpp")] + host[:2],
-                   check=True)
+    builds = [subprocess.Popen(flags + ["-o", str(hsc), os.path.join(REPO, "tests", "native", "host_san_check.cpp")]
+                               + host),
+              subprocess.Popen(flags + ["-o", str(planc), os.path.join(REPO, "tests", "native", "plan_check.cpp")]
+                               + host[:2])]
+    assert [b.wait() for b in builds] == [0, 0]
     scratch = tmp_path / "scratch"
     scratch.mkdir()
     out = subprocess.run([str(hsc), data_dir, str(scratch)], capture_output=True, text=True, env=env, timeout=600)
