@@ -68,6 +68,7 @@ struct kml_ctx {
   int device = 0;
   const char *bp_family = nullptr;  // kernel family of the last BP launch
   hipStream_t stream = nullptr;
+  hipStream_t cstream = nullptr;  // host-buffer frame uploads (kml_decode_frames' chunked path), made on first use
   kml::RunConfig rc;
   kml::LdpcCode code;
   kml::Modem modem;
@@ -875,6 +876,7 @@ void kml_destroy(kml_ctx *c) {
                     &c->w_pc, &c->w_cnt, &c->w_km, &c->s_synm, &c->s_synf, &c->s_itm, &c->s_itf, &c->s_Lm, &c->s_Lf, &c->s_list, &c->s_sel, &c->s_uu, &c->s_cc, &c->s_y, &c->s_h, &c->w_hc})
       b->release();
     hipStreamDestroy(c->stream);
+    if (c->cstream) hipStreamDestroy(c->cstream);
   }
   delete c;
 }
@@ -1122,12 +1124,91 @@ int kml_kmeans_dump_mat(const char *path, const double *data, int S, const doubl
   return (fclose(f) == 0 && ok) ? KML_OK : KML_E_IO;
 }
 
+namespace {
+// Codewords per chunk of the host-buffer known-channel path (KML_HOST_CHUNK;
+// 0 = one piece).
+int host_chunk() {
+  if (const char *e = getenv("KML_HOST_CHUNK")) return atoi(e);
+  return 8192;
+}
+
+// kml_decode_frames with HOST buffers and a known channel, in chunks: the
+// frames of chunk i + 1 cross PCIe on the copy stream while chunk i decodes on
+// the context's stream (which waits on the upload's event), and chunk i's
+// uu_hat / ret come back before chunk i + 1 is launched.  Chunks decode in
+// order on one stream, so every codeword sees what it sees in one call (the
+// known-channel decode has no cross-codeword state).  Only the transfers move.
+int decode_frames_chunked(kml_ctx *c, const double *y, const double *true_h, double snr, int B, uint8_t *uu_hat,
+                          int32_t *ret, int CH) {
+  const int S = c->code.cc_len / c->modem.bits, K = c->code.K;
+  const size_t ycw = (size_t)S * 2;  // doubles per codeword
+  HIPCHK(c, c->w_y.ensure((size_t)B * ycw * sizeof(double)), "hipMalloc(workspace)");
+  HIPCHK(c, c->w_h.ensure((size_t)B * 2 * sizeof(double)), "hipMalloc(workspace)");
+  HIPCHK(c, c->w_uh.ensure((size_t)B * K), "hipMalloc(workspace)");
+  if (ret) HIPCHK(c, c->w_ret.ensure((size_t)B * sizeof(int32_t)), "hipMalloc(workspace)");
+  if (!c->cstream) HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking), "hipStreamCreate");
+  const int n = (B + CH - 1) / CH;
+  std::vector<hipEvent_t> ev(n, nullptr);
+  int rc = KML_OK;
+  auto upload = [&](int i) -> int {
+    const size_t b0 = (size_t)i * CH, nb = std::min<size_t>(CH, B - b0);
+    HIPCHK(c, hipEventCreateWithFlags(&ev[i], hipEventDisableTiming), "hipEventCreate");
+    HIPCHK(c, hipMemcpyAsync(c->w_y.as<double>() + b0 * ycw, y + b0 * ycw, nb * ycw * sizeof(double),
+                             hipMemcpyHostToDevice, c->cstream), "H2D");
+    HIPCHK(c, hipMemcpyAsync(c->w_h.as<double>() + b0 * 2, true_h + b0 * 2, nb * 2 * sizeof(double),
+                             hipMemcpyHostToDevice, c->cstream), "H2D");
+    HIPCHK(c, hipEventRecord(ev[i], c->cstream), "hipEventRecord");
+    return KML_OK;
+  };
+  rc = upload(0);
+  for (int i = 0; i < n && rc == KML_OK; ++i) {
+    const size_t b0 = (size_t)i * CH;
+    const int nb = (int)std::min<size_t>(CH, B - b0);
+    if (hipStreamWaitEvent(c->stream, ev[i], 0) != hipSuccess) {
+      rc = fail(c, KML_E_HIP, "hipStreamWaitEvent");
+      break;
+    }
+    RecvIO io;
+    io.y = reinterpret_cast<const double2 *>(c->w_y.as<double>() + b0 * ycw);
+    io.true_h = reinterpret_cast<const double2 *>(c->w_h.as<double>() + b0 * 2);
+    io.uh = c->w_uh.as<uint8_t>() + b0 * K;
+    io.ret = ret ? c->w_ret.as<int32_t>() + b0 : nullptr;
+    int slot;
+    if ((rc = receive(c, io, snr, nb, slot)) != KML_OK) break;
+    if (i + 1 < n && (rc = upload(i + 1)) != KML_OK) break;  // overlaps chunk i's decode
+    if (hipMemcpyAsync(uu_hat + b0 * K, io.uh, (size_t)nb * K, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        (ret && hipMemcpyAsync(ret + b0, io.ret, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, c->stream) != hipSuccess)) {
+      rc = fail(c, KML_E_HIP, "D2H");
+      break;
+    }
+  }
+  if (rc != KML_OK) {  // leave no upload in flight into the workspaces
+    hipStreamSynchronize(c->cstream);
+    hipStreamSynchronize(c->stream);
+  } else {
+    rc = sync(c);
+  }
+  for (hipEvent_t e : ev)
+    if (e) hipEventDestroy(e);
+  return rc;
+}
+}  // namespace
+
 int kml_decode_frames(kml_ctx *c, const double *y, const double *true_h, double snr, int B, uint8_t *uu_hat,
                       int32_t *chosen, double *metrics, int32_t *ret, double *h_hat, int flags) {
   if (!c || !y || !uu_hat || B < 0) return fail(c, KML_E_ARG, "kml_decode_frames: bad argument");
   if (B == 0) return KML_OK;
   TRY(need_gpu(c));
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  if (true_h && !(flags & (KML_DEVICE_PTRS | KML_HISTOGRAM))) {
+    const int CH = host_chunk();
+    if (CH > 0 && B > CH) {
+      if (chosen) memset(chosen, 0, sizeof(int32_t) * B);  // single candidate (kmcodec.cc:66-67)
+      if (metrics) memset(metrics, 0, sizeof(double) * 4 * B);
+      if (h_hat) memset(h_hat, 0, sizeof(double) * 2 * B);
+      return decode_frames_chunked(c, y, true_h, snr, B, uu_hat, ret, CH);
+    }
+  }
   const int S = c->code.cc_len / c->modem.bits;
   const double *d_y, *d_h = nullptr;
   TRY(stage_in(c, c->w_y, y, (size_t)B * S * 2, flags, d_y));
