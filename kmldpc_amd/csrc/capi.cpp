@@ -1132,20 +1132,25 @@ int host_chunk() {
   return 8192;
 }
 
-// kml_decode_frames with HOST buffers and a known channel, in chunks: the
-// frames of chunk i + 1 cross PCIe on the copy stream while chunk i decodes on
-// the context's stream (which waits on the upload's event), and chunk i's
-// uu_hat / ret come back before chunk i + 1 is launched.  Chunks decode in
-// order on one stream, so every codeword sees what it sees in one call (the
-// known-channel decode has no cross-codeword state).  Only the transfers move.
+// kml_decode_frames with HOST buffers, in chunks: the frames of chunk i + 1
+// cross PCIe on the copy stream while chunk i decodes on the context's stream
+// (which waits on the upload's event), and chunk i's outputs come back before
+// chunk i + 1 is launched.  Chunks decode in order on one stream, so every
+// codeword sees what it sees in one call: the known-channel and hard-metric
+// decodes have no cross-codeword state (the soft metric's stale syndrom_soft_
+// has; its calls stay in one piece).  Only the transfers move.  chosen /
+// metrics / h_hat are the blind path's outputs (NULL on the known path).
 int decode_frames_chunked(kml_ctx *c, const double *y, const double *true_h, double snr, int B, uint8_t *uu_hat,
-                          int32_t *ret, int CH) {
+                          int32_t *chosen, double *metrics, int32_t *ret, double *h_hat, int CH) {
   const int S = c->code.cc_len / c->modem.bits, K = c->code.K;
   const size_t ycw = (size_t)S * 2;  // doubles per codeword
   HIPCHK(c, c->w_y.ensure((size_t)B * ycw * sizeof(double)), "hipMalloc(workspace)");
-  HIPCHK(c, c->w_h.ensure((size_t)B * 2 * sizeof(double)), "hipMalloc(workspace)");
+  if (true_h) HIPCHK(c, c->w_h.ensure((size_t)B * 2 * sizeof(double)), "hipMalloc(workspace)");
   HIPCHK(c, c->w_uh.ensure((size_t)B * K), "hipMalloc(workspace)");
   if (ret) HIPCHK(c, c->w_ret.ensure((size_t)B * sizeof(int32_t)), "hipMalloc(workspace)");
+  if (chosen) HIPCHK(c, c->w_sel.ensure((size_t)B * sizeof(int32_t)), "hipMalloc(workspace)");
+  if (metrics) HIPCHK(c, c->w_met.ensure((size_t)B * 4 * sizeof(double)), "hipMalloc(workspace)");
+  if (h_hat) HIPCHK(c, c->w_hhat.ensure((size_t)B * 2 * sizeof(double)), "hipMalloc(workspace)");
   if (!c->cstream) HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking), "hipStreamCreate");
   const int n = (B + CH - 1) / CH;
   std::vector<hipEvent_t> ev(n, nullptr);
@@ -1155,8 +1160,9 @@ int decode_frames_chunked(kml_ctx *c, const double *y, const double *true_h, dou
     HIPCHK(c, hipEventCreateWithFlags(&ev[i], hipEventDisableTiming), "hipEventCreate");
     HIPCHK(c, hipMemcpyAsync(c->w_y.as<double>() + b0 * ycw, y + b0 * ycw, nb * ycw * sizeof(double),
                              hipMemcpyHostToDevice, c->cstream), "H2D");
-    HIPCHK(c, hipMemcpyAsync(c->w_h.as<double>() + b0 * 2, true_h + b0 * 2, nb * 2 * sizeof(double),
-                             hipMemcpyHostToDevice, c->cstream), "H2D");
+    if (true_h)
+      HIPCHK(c, hipMemcpyAsync(c->w_h.as<double>() + b0 * 2, true_h + b0 * 2, nb * 2 * sizeof(double),
+                               hipMemcpyHostToDevice, c->cstream), "H2D");
     HIPCHK(c, hipEventRecord(ev[i], c->cstream), "hipEventRecord");
     return KML_OK;
   };
@@ -1170,14 +1176,23 @@ int decode_frames_chunked(kml_ctx *c, const double *y, const double *true_h, dou
     }
     RecvIO io;
     io.y = reinterpret_cast<const double2 *>(c->w_y.as<double>() + b0 * ycw);
-    io.true_h = reinterpret_cast<const double2 *>(c->w_h.as<double>() + b0 * 2);
+    io.true_h = true_h ? reinterpret_cast<const double2 *>(c->w_h.as<double>() + b0 * 2) : nullptr;
     io.uh = c->w_uh.as<uint8_t>() + b0 * K;
     io.ret = ret ? c->w_ret.as<int32_t>() + b0 : nullptr;
+    io.chosen = chosen ? c->w_sel.as<int32_t>() + b0 : nullptr;
+    io.met = metrics ? c->w_met.as<double>() + b0 * 4 : nullptr;
+    io.hhat = h_hat ? reinterpret_cast<double2 *>(c->w_hhat.as<double>() + b0 * 2) : nullptr;
     int slot;
     if ((rc = receive(c, io, snr, nb, slot)) != KML_OK) break;
     if (i + 1 < n && (rc = upload(i + 1)) != KML_OK) break;  // overlaps chunk i's decode
     if (hipMemcpyAsync(uu_hat + b0 * K, io.uh, (size_t)nb * K, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        (ret && hipMemcpyAsync(ret + b0, io.ret, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, c->stream) != hipSuccess)) {
+        (ret && hipMemcpyAsync(ret + b0, io.ret, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, c->stream) != hipSuccess) ||
+        (chosen && hipMemcpyAsync(chosen + b0, io.chosen, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, c->stream) !=
+                       hipSuccess) ||
+        (metrics && hipMemcpyAsync(metrics + b0 * 4, io.met, sizeof(double) * 4 * nb, hipMemcpyDeviceToHost,
+                                   c->stream) != hipSuccess) ||
+        (h_hat && hipMemcpyAsync(h_hat + b0 * 2, io.hhat, sizeof(double) * 2 * nb, hipMemcpyDeviceToHost, c->stream) !=
+                      hipSuccess)) {
       rc = fail(c, KML_E_HIP, "D2H");
       break;
     }
@@ -1200,13 +1215,14 @@ int kml_decode_frames(kml_ctx *c, const double *y, const double *true_h, double 
   if (B == 0) return KML_OK;
   TRY(need_gpu(c));
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
-  if (true_h && !(flags & (KML_DEVICE_PTRS | KML_HISTOGRAM))) {
+  if (!(flags & (KML_DEVICE_PTRS | KML_HISTOGRAM)) && (true_h || !c->rc.metric_soft)) {
     const int CH = host_chunk();
     if (CH > 0 && B > CH) {
+      if (!true_h) return decode_frames_chunked(c, y, nullptr, snr, B, uu_hat, chosen, metrics, ret, h_hat, CH);
       if (chosen) memset(chosen, 0, sizeof(int32_t) * B);  // single candidate (kmcodec.cc:66-67)
       if (metrics) memset(metrics, 0, sizeof(double) * 4 * B);
       if (h_hat) memset(h_hat, 0, sizeof(double) * 2 * B);
-      return decode_frames_chunked(c, y, true_h, snr, B, uu_hat, ret, CH);
+      return decode_frames_chunked(c, y, true_h, snr, B, uu_hat, nullptr, nullptr, ret, nullptr, CH);
     }
   }
   const int S = c->code.cc_len / c->modem.bits;

@@ -716,15 +716,16 @@ def test_gpu_encoder_equals_host_encoder(data_dir, matrix, modem, is5g):
     assert np.array_equal(cc_gpu, cc_host)
 
 
+@pytest.mark.parametrize("blind", [False, True])
 @pytest.mark.parametrize("matrix,modem,is5g", [("PEG2304regular0.5.txt", "2bits_QPSK.txt", False),
                                                ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True),
                                                ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False)])
-def test_host_buffer_chunked_decode_matches_one_piece(data_dir, matrix, modem, is5g, monkeypatch):
-    """kml_decode_frames with host buffers and a known channel uploads the
-    frames in chunks on a copy stream while the previous chunk decodes
-    (KML_HOST_CHUNK codewords per chunk): with small chunks and a ragged last
-    chunk every output equals the one-piece call (KML_HOST_CHUNK=0), and
-    sampled codewords equal the oracle."""
+def test_host_buffer_chunked_decode_matches_one_piece(data_dir, matrix, modem, is5g, blind, monkeypatch):
+    """kml_decode_frames with host buffers (known channel, or blind with the
+    hard metric) uploads the frames in chunks on a copy stream while the
+    previous chunk decodes (KML_HOST_CHUNK codewords per chunk): with small
+    chunks and a ragged last chunk every output equals the one-piece call
+    (KML_HOST_CHUNK=0), and sampled codewords equal the oracle."""
     ctx = ctx_for(data_dir, matrix, modem, is5g, max_iter=50 if is5g else 20)
     oc = oracle_for(data_dir, matrix, is5g, max_iter=50 if is5g else 20)
     om = O.Modem(os.path.join(data_dir, modem))
@@ -732,11 +733,13 @@ def test_host_buffer_chunked_decode_matches_one_piece(data_dir, matrix, modem, i
     uu, cc, th, y = O.gen_frames(oc, om, 5.0 if is5g else 2.0, B, state=31)
     snr = 5.0 if is5g else 2.0
     monkeypatch.setenv("KML_HOST_CHUNK", "0")
-    r0 = ctx.decode_frames(y, snr, th)
+    r0 = ctx.decode_frames(y, snr, None if blind else th)
     monkeypatch.setenv("KML_HOST_CHUNK", "16")
-    r1 = ctx.decode_frames(y, snr, th)
+    r1 = ctx.decode_frames(y, snr, None if blind else th)
     for k in ("uu_hat", "chosen", "ret", "metrics", "h_hat"):
         assert np.array_equal(r1[k], r0[k]), k
     for i in (0, 15, 16, 47, 48, 60):
-        ref = O.receive(oc, om, y[i], th[i], snr, False)
+        ref = O.receive(oc, om, y[i], th[i], snr, blind)
         assert np.array_equal(r1["uu_hat"][i], ref["uu_hat"]) and r1["ret"][i] == ref["ret"], i
+        if blind:
+            assert r1["chosen"][i] == ref["chosen"], i
