@@ -149,14 +149,65 @@ def cpu_baseline(d, args):
                 break
     except OSError:
         pass
-    return {"value": round(r["cw_per_s"], 3), "unit": "codewords/s", "cores": threads, "kind": "port",
-            "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
-            "full_loop_value": round(r["full_loop_cw_per_s"], 3),
-            "sample": f"{r['codewords']} codewords ({n}/thread x {threads} threads, one Park-Miller stream per "
-                      f"thread) of the same workload through oracle/ (C restatement of KmCodec::Decoder + CntErr, "
-                      f"bit-exact vs reference): decode {r['seconds']:.1f} s (value), + frame generation "
-                      f"{r['gen_seconds']:.1f} s (full_loop_value); FER {r['fer']:.4f}",
-            "cpu_model": cpu_model}
+    ncw = r["codewords"]
+    fer, ber = r["fer"], r["ber"]
+    mean_e = r["err_bit"] / ncw
+    ber_sig = (math.sqrt(max(r["sum_e2"] / ncw - mean_e * mean_e, 0.0) * ncw / max(ncw - 1, 1) / ncw) / r["K"]
+               if ncw > 1 else None)
+    out = {"value": round(r["cw_per_s"], 3), "unit": "codewords/s", "cores": threads, "kind": "port",
+           "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+           "full_loop_value": round(r["full_loop_cw_per_s"], 3),
+           "sample": f"{ncw} codewords ({n}/thread x {threads} threads, one Park-Miller stream per "
+                     f"thread) of the same workload through oracle/ (C restatement of KmCodec::Decoder + CntErr, "
+                     f"bit-exact vs reference): decode {r['seconds']:.1f} s (value), + frame generation "
+                     f"{r['gen_seconds']:.1f} s (full_loop_value)",
+           # the baseline's BER/FER with 1 sigma (FER binomial; BER over codewords, whose bit
+           # errors are dependent)
+           "fer": round(fer, 6), "fer_sigma": round(math.sqrt(fer * (1 - fer) / ncw), 6),
+           "ber": round(ber, 8), "ber_sigma": round(ber_sig, 8) if ber_sig is not None else None,
+           "cpu_model": cpu_model}
+    out["single_core"] = single_core_rates(d, args, exe)
+    return out
+
+
+def single_core_rates(d, args, exe):
+    """One core: the reference itself (oracle/_ref/ref_harness: the reference's
+    own sources, its sequential seed-17 stream, construction excluded) beside
+    the restatement (oracle/cpu_baseline, 1 thread) on the same workload; both
+    decode-only (frames generated outside the timed loop) and full-loop rates.
+    A bounded sample of about args.ref_seconds each."""
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    per_core = 250.0 if args.blind else 500.0
+    if args.matrix.startswith("PEG8064") or args.is5g:
+        per_core = 30.0 if args.matrix.startswith("PEG8064") else 130.0
+    n = max(20, int(args.ref_seconds * per_core))
+    res = {"codewords": n}
+    try:
+        cmd = [exe, os.path.join(d, args.matrix), os.path.join(d, args.modem), str(int(args.is5g)), repr(args.snr),
+               str(args.max_iter), str(int(args.blind)), str(n), "1"]
+        pr = json.loads(subprocess.run(cmd, capture_output=True, text=True, timeout=600).stdout.strip().splitlines()[-1])
+        res["port"] = {"value": round(pr["cw_per_s"], 3), "full_loop_value": round(pr["full_loop_cw_per_s"], 3),
+                       "what": "oracle/cpu_baseline, 1 thread, own Park-Miller stream"}
+    except Exception as e:  # pragma: no cover
+        res["port"] = f"failed: {e}"
+    if not os.path.exists(harness):
+        res["reference"] = "oracle/_ref/ref_harness not built (needs /root/reference at build time)"
+        return res
+    try:
+        out = os.path.join(d, "ref_sim.bin")
+        rr = subprocess.run([harness, os.path.join(d, "config.toml"), repr(args.snr), str(n), out, "simulate"],
+                            capture_output=True, text=True, timeout=900, cwd=d)
+        t = json.loads([ln for ln in rr.stderr.splitlines() if ln.startswith('{"codewords"')][-1])
+        rx, gen = t["receive_seconds"], t["gen_seconds"]
+        res["reference"] = {"value": round(n / rx, 3), "full_loop_value": round(n / (rx + gen), 3),
+                            "what": "oracle/_ref/ref_harness simulate mode: the reference's KmCodec::Decoder + "
+                                    "k-means + SourceSink::CntErr on its own seed-17 stream, 1 core, construction "
+                                    "excluded; value = receive only, full_loop_value = + source/encoder/channel"}
+        if isinstance(res.get("port"), dict):
+            res["port_over_reference"] = round(res["port"]["value"] / res["reference"]["value"], 3)
+    except Exception as e:  # pragma: no cover
+        res["reference"] = f"failed: {e}"
+    return res
 
 
 def free_port():
@@ -243,15 +294,20 @@ def main():
     ap.add_argument("--seed", type=int, default=17)
     ap.add_argument("--cpu-cw-per-thread", type=int, default=0, help="0: sized for --cpu-seconds")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--ref-seconds", type=float, default=6.0,
+                    help="single-core samples (reference and restatement) of about this many seconds each")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ber-match", action="store_true")
     ap.add_argument("--full-loop-batches", type=int, default=3)
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run under torch.distributed.run and build the process group (init, all_reduce, "
+                         "all_gather) even for --gpus 1: a 1-rank RCCL group")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI, the production path) or gloo (CPU counters; lets N ranks share "
                          "fewer GPUs for testing)")
     args = ap.parse_args()
 
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if (args.gpus > 1 or args.force_dist) and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
 
     global K
@@ -267,7 +323,7 @@ def main():
     dist = None
     device = local
     ranks_seen = 1
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch
         import torch.distributed as dist_mod
 
@@ -452,8 +508,9 @@ def main():
             "global_batch": B * world,
             "parallelism": f"codeword-sharded x{world}",
         },
-        "dist_backend": args.dist_backend if world > 1 else None,
-        "rccl_ranks": ranks_seen if (world > 1 and args.dist_backend == "nccl") else (1 if world == 1 else None),
+        "dist_backend": args.dist_backend if dist is not None else None,
+        # ranks of the RCCL process group (0: no process group, or gloo)
+        "rccl_ranks": ranks_seen if (dist is not None and args.dist_backend == "nccl") else 0,
         "ranks": ranks_seen,
         "rank_ms_per_step": [round(t / args.steps * 1e3, 3) for t in per_rank],
         "full_loop": {

@@ -157,7 +157,9 @@ int kml_decode_frames(kml_ctx *ctx, const double *y, const double *true_h, doubl
  * nc > 1 computes every candidate's syndrome metric (hard PEG count, 5G
  * metric_iter BP count, or the soft metric, as configured), takes the first
  * minimum, demaps with it and decodes.  chosen[B], metrics[B][4] (entries
- * >= nc are 0), ret[B] may be NULL.  KML_HISTOGRAM: metrics only. */
+ * >= nc are 0), ret[B] may be NULL.  KML_HISTOGRAM: metrics only
+ * (KmCodec::GetHistogramData, kmcodec.cc:75-79), for nc == 1 too: the single
+ * candidate's metric, no final decode, ret zeroed. */
 int kml_decode_candidates(kml_ctx *ctx, const double *y, const double *h_hats, int nc, double snr, int B,
                           uint8_t *uu_hat, int32_t *chosen, double *metrics, int32_t *ret, int flags);
 
@@ -275,6 +277,11 @@ int kml_log_probe(kml_ctx *ctx, const double *in, int n, double *out);
  * CN-phase n0/s, CN-phase n1/s (near-one reciprocal), the near-one reciprocal
  * formula of s, hipcc's refined reciprocal of s) — see bp_common.hpp. */
 int kml_div_probe(kml_ctx *ctx, const double *in, int n, double *out);
+/* Test hook: after the nth (0-based) cooperative BP launch from now, set that
+ * kernel's abort word as a timed-out group barrier would (nth < 0: off).  The
+ * call that owns the launch must then fail with KML_E_HIP, even when later
+ * launches of the same call (chunks of a host-buffer decode) follow it. */
+int kml_debug_inject_abort(kml_ctx *ctx, int nth);
 
 #ifdef __cplusplus
 }

@@ -68,6 +68,14 @@ class GpuLdpcCodec : public Base {
       : Base(args), ctx_(open_ctx(config_path, device)) {
     check(ctx_, kml_dims(ctx_, dims_));
   }
+  // From an existing CPU codec (the reference's copy constructor, binaryldpccodec.h:14):
+  // skips a second H load + SystemMatrixH elimination, which takes about a minute
+  // on one core for PEG8064.  (Not for Binary5GLDPCCodec, whose copy the
+  // reference itself avoids: kmcodec.cc:8-11.)
+  GpuLdpcCodec(const Base &cpu, const std::string &config_path, int device = 0)
+      : Base(cpu), ctx_(open_ctx(config_path, device)) {
+    check(ctx_, kml_dims(ctx_, dims_));
+  }
   GpuLdpcCodec(const GpuLdpcCodec &) = delete;
   GpuLdpcCodec &operator=(const GpuLdpcCodec &) = delete;
   ~GpuLdpcCodec() override { kml_destroy(ctx_); }

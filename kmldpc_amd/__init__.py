@@ -95,6 +95,7 @@ def lib():
         "kml_prof_read_flops": (I, [P, C.c_char_p, P]),
         "kml_math_probe": (I, [P, P, I, P]),
         "kml_div_probe": (I, [P, P, I, P]),
+        "kml_debug_inject_abort": (I, [P, I]),
         "kml_log_probe": (I, [P, P, I, P]),
         "kml_lcg_uniform": (D, [P]),
         "kml_lcg_normal": (None, [P, P, I]),
@@ -376,6 +377,10 @@ class Context:
         out = np.zeros((x.shape[0], 8))
         self._chk(lib().kml_div_probe(self._h, _p(x), x.shape[0], _p(out)), "kml_div_probe")
         return out
+
+    def debug_inject_abort(self, nth):
+        """Test hook: raise the abort word after the nth cooperative BP launch."""
+        self._chk(lib().kml_debug_inject_abort(self._h, int(nth)), "kml_debug_inject_abort")
 
     def ref_frames(self, rng, snr, n):
         """n frames of the reference's sequential stream (Simulator::run_blocks)

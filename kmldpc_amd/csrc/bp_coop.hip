@@ -840,6 +840,17 @@ __device__ __forceinline__ unsigned hi_of(unsigned long long w) { return (unsign
 // Mailbox accesses through a buffer resource (SGPRs) and 32-bit byte offsets:
 // no 64-bit per-lane addresses to keep live across the phases.  Polls load
 // with sc1 (L2-served, bypassing the never-refreshed vector L1).
+// Hardware assumption (the tag protocol's only one): a naturally aligned 8-byte
+// word written by one b64 / b128 store is read whole by one b64 / b128 load —
+// no load returns a new high dword (the tag) with a stale low dword.  Each
+// 8-byte word carries its own tag, so nothing wider than 8 bytes must be
+// single-copy atomic.  This is the property the AMDGPU backend itself relies on
+// when it lowers a relaxed 64-bit atomic load / store to a plain dwordx2
+// access.  A 16-byte entry is 16-byte aligned, so it never straddles a
+// 128-byte L2 line and reaches the L2 as one request.  All members of a
+// group run on one XCD (same_xcd: the tagged launch defers every other group's
+// codewords to the barrier-exchange launch), so producer and consumer share
+// that L2 and no cross-XCD coherence is involved.
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBufFlags = 0x00020000;  // gfx9 raw buffer resource, dword 3
@@ -1478,8 +1489,8 @@ hipError_t launch_coop_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int
   auto kern = bp_coop_kernel<kG, T, RV, RC, SYN>;
   hipError_t e = hipMemsetAsync(a.queue, 0, sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
-  // group blocks + the abort word
-  e = hipMemsetAsync(a.gsync, 0, sizeof(GroupSync) * (size_t)groups + sizeof(unsigned), s);
+  // group blocks, and the abort word unless an unchecked earlier launch may have set it
+  e = hipMemsetAsync(a.gsync, 0, sizeof(GroupSync) * (size_t)groups + (a.reset_abort ? sizeof(unsigned) : 0), s);
   if (e != hipSuccess) return e;
   DevCode cc = c;
   BpLaunch aa = a;
@@ -1590,8 +1601,8 @@ hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s) {
 #define KML_PART_CASE(T_, R_, X_)                                                                   \
   if (k.T == T_ && xmax <= X_ * T_) {                                                              \
     if (tagged) {                                                                                  \
-      hipError_t e = a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true, true>(c, d, s, fast, groups, true)    \
-                           : launch_part_t<kPartG, T_, R_, R_, X_, false, true>(c, d, s, fast, groups, true);  \
+      hipError_t e = a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true, true>(c, d, s, fast, groups, a.reset_abort)   \
+                           : launch_part_t<kPartG, T_, R_, R_, X_, false, true>(c, d, s, fast, groups, a.reset_abort); \
       if (e != hipSuccess) return e;                                                               \
       BpLaunch b = a;                                                                              \
       b.cw_idx = d.defer_idx;                                                                      \
@@ -1599,8 +1610,8 @@ hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s) {
       return a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true, false>(c, b, s, fast, groups, false)          \
                    : launch_part_t<kPartG, T_, R_, R_, X_, false, false>(c, b, s, fast, groups, false);        \
     }                                                                                              \
-    return a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true, false>(c, a, s, fast, groups, true)             \
-                 : launch_part_t<kPartG, T_, R_, R_, X_, false, false>(c, a, s, fast, groups, true);           \
+    return a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true, false>(c, a, s, fast, groups, a.reset_abort)    \
+                 : launch_part_t<kPartG, T_, R_, R_, X_, false, false>(c, a, s, fast, groups, a.reset_abort);  \
   }
     KML_PART_CASE(512, 4, 4)
     KML_PART_CASE(768, 3, 3)
@@ -1618,6 +1629,10 @@ hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s) {
   KML_COOP_CASE(8, 1024, 1)
 #undef KML_COOP_CASE
   return hipErrorNotSupported;
+}
+
+hipError_t bp_coop_raise_abort(const BpLaunch &a, int groups, hipStream_t s) {
+  return hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(reinterpret_cast<GroupSync *>(a.gsync) + groups), 1u, 1, s);
 }
 
 // Did the last cooperative launch abort (a group barrier timed out)?

@@ -85,6 +85,7 @@ struct kml_ctx {
   int coop_groups = 0;      // cooperative BP groups (0: kernel not used)
   long long part_cut = 0;   // cut edges of the partition plan (partitioned cooperative kernel)
   bool coop_pending = false;  // a cooperative launch whose abort word is unchecked
+  int inject_abort = -1;      // test hook (kml_debug_inject_abort): raise the abort after the n-th coop launch
   // workspaces
   DBuf w_y, w_h, w_h4, w_hhat, w_p0, w_uu, w_uh, w_uh4, w_ret, w_cch, w_syn, w_sel, w_met, w_pc, w_cnt, w_km, w_cwerr;
   // soft syndrome metric: candidate / final syndromes, iteration counts, sums, decode lists
@@ -389,12 +390,18 @@ int run_bp(kml_ctx *c, kml::BpLaunch a, int &slot_out, int reuse = -1) {
   a.queue = c->d_queue.as<unsigned int>();
   a.gsync = c->d_gsync.p;
   a.gcch = c->d_gcch.as<uint8_t>();
+  // the abort word is cleared only by the first cooperative launch after the
+  // last sync(): a timeout in any launch before the check (e.g. chunk 0 of a
+  // chunked host-buffer call) stays set until sync() reports it
+  a.reset_abort = !c->coop_pending;
   if (c->coop_groups > 0) c->coop_pending = true;
   Timer t(c, "bp", slot, (double)a.B * 8.0 * c->code.cc_len);
   const char *msg = nullptr;
   hipError_t e = kml::launch_bp(c->dc, a, c->stream, &msg, &c->bp_family);
   t.stop();
   if (e != hipSuccess) return msg ? fail(c, KML_E_UNSUP, msg) : hip_fail(c, e, "bp launch");
+  if (c->inject_abort >= 0 && c->coop_groups > 0 && c->inject_abort-- == 0)  // as if a group barrier timed out
+    HIPCHK(c, kml::bp_coop_raise_abort(a, c->coop_groups, c->stream), "inject abort");
   slot_out = slot;
   return KML_OK;
 }
@@ -1209,6 +1216,12 @@ int decode_frames_chunked(kml_ctx *c, const double *y, const double *true_h, dou
 }
 }  // namespace
 
+int kml_debug_inject_abort(kml_ctx *c, int nth) {
+  if (!c) return KML_E_ARG;
+  c->inject_abort = nth;
+  return KML_OK;
+}
+
 int kml_decode_frames(kml_ctx *c, const double *y, const double *true_h, double snr, int B, uint8_t *uu_hat,
                       int32_t *chosen, double *metrics, int32_t *ret, double *h_hat, int flags) {
   if (!c || !y || !uu_hat || B < 0) return fail(c, KML_E_ARG, "kml_decode_frames: bad argument");
@@ -1274,8 +1287,10 @@ int kml_decode_candidates(kml_ctx *c, const double *y, const double *h_hats, int
                           uint8_t *uu_hat, int32_t *chosen, double *metrics, int32_t *ret, int flags) {
   if (!c || !y || !h_hats || !uu_hat || B < 0 || nc < 1 || nc > 4)
     return fail(c, KML_E_ARG, "kml_decode_candidates: bad argument (need 1 <= nc <= 4)");
-  if (nc == 1)  // one estimate: no metric (kmcodec.cc:66-67)
-    return kml_decode_frames(c, y, h_hats, snr, B, uu_hat, chosen, metrics, ret, nullptr, flags & ~KML_HISTOGRAM);
+  // one estimate: Decoder computes no metric (kmcodec.cc:66-67); GetHistogramData
+  // (kmcodec.cc:75-79, KML_HISTOGRAM) computes that candidate's metric, as the
+  // known-channel histogram path of kml_decode_frames does
+  if (nc == 1) return kml_decode_frames(c, y, h_hats, snr, B, uu_hat, chosen, metrics, ret, nullptr, flags);
   if (B == 0) return KML_OK;
   TRY(need_gpu(c));
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");

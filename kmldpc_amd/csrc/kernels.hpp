@@ -82,6 +82,10 @@ struct BpLaunch {
   double2 *gslots = nullptr;     // global slot scratch when E*16 exceeds LDS
   long long gslots_cap = 0;      // number of double2 available
   unsigned int *queue = nullptr; // 4-byte device dequeue counter (zeroed by the launcher)
+  // Cooperative kernels: clear the abort word before the launch.  The caller
+  // clears it only for the first launch after the last check (capi.cpp sync),
+  // so a timeout in an earlier launch of the same API call stays visible.
+  bool reset_abort = true;
   // Fused demap (bp_regular.hip only, bp_regular_fuses_demap): when sym_y is
   // set, p0 is ignored and each codeword's P0 is computed in the kernel's
   // prologue from y[B][S] and the known channel h[B] (demap_common.hpp).
@@ -112,6 +116,8 @@ bool part_plan_fits(int N, int M, int E, int ncut, int mirror_max, int xmax);
 // Name of the cooperative kernel launch_bp_coop runs for this code.
 const char *bp_coop_family(const DevCode &c);
 bool bp_coop_aborted(const BpLaunch &a, int groups, hipStream_t s);
+// Test hook: set the abort word on the stream, as a timed-out group barrier would.
+hipError_t bp_coop_raise_abort(const BpLaunch &a, int groups, hipStream_t s);
 // Threads per workgroup of the regular kernel for this code shape, 0 if it does
 // not apply (host-side; decides whether upload_code builds the LDS plan).
 int bp_regular_threads(int N, int M, int E, int dv_max, int dc_max, int regular);

@@ -1066,15 +1066,15 @@ __global__ __launch_bounds__(256) void km_state_kernel(const double *__restrict_
                                                        int S, const double2 *__restrict__ hat,
                                                        double2 *__restrict__ clusters, int *__restrict__ idx) {
   __shared__ double2 cl[KC];
-  const int cw = blockIdx.y;
+  const int cw = blockIdx.x;  // codewords in x (up to 2^31 - 1), symbol blocks in y
   const cplx h{hat[cw].x, hat[cw].y};
   for (int k = threadIdx.x; k < KC; k += blockDim.x) {
     const cplx p = kml_cmul(cplx{cons[2 * k], cons[2 * k + 1]}, h);  // kmeans.cc:72-74
     cl[k] = make_double2(p.re, p.im);
-    if (blockIdx.x == 0 && clusters) clusters[(long long)cw * KC + k] = cl[k];
+    if (blockIdx.y == 0 && clusters) clusters[(long long)cw * KC + k] = cl[k];
   }
   __syncthreads();
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = blockIdx.y * blockDim.x + threadIdx.x;
   if (j >= S || !idx) return;
   const double2 v = y[(long long)cw * S + j];
   idx[(long long)cw * S + j] = first_argmin<KC>(cl, v.x, v.y);
@@ -1084,7 +1084,8 @@ __global__ __launch_bounds__(256) void km_state_kernel(const double *__restrict_
 hipError_t launch_kmeans_state(int Kc, const double *cons, const double2 *y, int S, int B, const double2 *hat,
                                double2 *clusters, int *idx, hipStream_t s) {
   if (B == 0) return hipSuccess;
-  const dim3 grid((S + 255) / 256, B), blk(256);
+  if ((S + 255) / 256 > 65535) return hipErrorInvalidValue;
+  const dim3 grid(B, (S + 255) / 256), blk(256);
   switch (Kc) {
     case 2: hipLaunchKernelGGL(km_state_kernel<2>, grid, blk, 0, s, cons, y, S, hat, clusters, idx); break;
     case 4: hipLaunchKernelGGL(km_state_kernel<4>, grid, blk, 0, s, cons, y, S, hat, clusters, idx); break;

@@ -48,7 +48,9 @@ extern "C" int kml_sweep_point(const kml_point_cfg *cfg, kml_batch_fn decode, vo
     for (long long j = 0; j < mine; j++) my_eb += err[j] > 0;
     std::fill(v.begin(), v.end(), 0);
     v[r] = my_eb;
-    if (W > 1 && (rc = reduce(v.data(), W, ruser)) != KML_OK) break;
+    // a 1-rank world still reduces when the caller passes a reducer (an identity
+    // all-reduce; exercises a 1-rank RCCL process group)
+    if (reduce && (rc = reduce(v.data(), W, ruser)) != KML_OK) break;
     uint64_t before = eblk;
     for (int q = 0; q < r; q++) before += v[q];
     // this rank's codewords in global order, with the per-codeword stop check
@@ -74,7 +76,7 @@ extern "C" int kml_sweep_point(const kml_point_cfg *cfg, kml_batch_fn decode, vo
       }
     }
     uint64_t loc[4] = {l_ebit, l_eb, take * K, take};
-    if (W > 1 && (rc = reduce(loc, 4, ruser)) != KML_OK) break;
+    if (reduce && (rc = reduce(loc, 4, ruser)) != KML_OK) break;
     ebit += loc[0];
     eblk += loc[1];
     tbit += loc[2];

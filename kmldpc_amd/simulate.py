@@ -104,7 +104,7 @@ class Simulator:
             hist = f"histogram_{snr:f}.txt" if self.world == 1 else f"histogram_{snr:f}.rank{self.rank}.txt"
         c = self.ctx.sim_point(snr, point_seed(self.seed, i), rank=self.rank, world=self.world, batch=self.batch,
                                max_blocks=max(rc["maximum_block_number"], 0), max_err=max(rc["maximum_error_number"], 0),
-                               hist_path=hist, reduce=self._reduce if self.world > 1 else None,
+                               hist_path=hist, reduce=self._reduce if self.dist is not None else None,
                                report=lambda v: self.log.info(result_line(snr, v)))
         v = [c["err_bit"], c["err_blk"], c["tot_bit"], c["tot_blk"]]
         self.log.info(result_line(snr, v))
@@ -136,6 +136,9 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=int(os.environ.get("KML_SEED", "0")))
     ap.add_argument("--dist-backend", default=os.environ.get("KML_DIST_BACKEND", "nccl"),
                     help="nccl (RCCL over xGMI, one GPU per rank) or gloo (CPU counters; ranks may share a GPU)")
+    ap.add_argument("--force-dist", action="store_true", default=os.environ.get("KML_FORCE_DIST", "") == "1",
+                    help="build the process group (and run its all-reduces) even when WORLD_SIZE is 1, "
+                         "e.g. a 1-rank RCCL group under torchrun --nproc-per-node 1")
     args = ap.parse_args(argv)
     t0 = time.monotonic()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -149,7 +152,7 @@ def main(argv=None):
         return 0
     lib()  # the HIP library (and its ROCm runtime) before torch
     dist = None
-    if world > 1:
+    if world > 1 or (args.force_dist and "WORLD_SIZE" in os.environ):
         import torch
         import torch.distributed as dist_mod
         if args.dist_backend == "nccl":

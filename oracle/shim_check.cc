@@ -52,9 +52,10 @@ int main(int argc, char **argv) {
   if (is5g) {
     ref_bp.reset(new lab::Binary5GLDPCCodec(args));
     gpu_bp.reset(new kml_lab::GpuBinary5GLDPCCodec(args, cfg, 0));
-  } else {
-    ref_bp.reset(new lab::BinaryLDPCCodec(args));
-    gpu_bp.reset(new kml_lab::GpuBinaryLDPCCodec(args, cfg, 0));
+  } else {  // the GPU codec copies the CPU one (no second SystemMatrixH elimination)
+    auto *cpu = new lab::BinaryLDPCCodec(args);
+    ref_bp.reset(cpu);
+    gpu_bp.reset(new kml_lab::GpuBinaryLDPCCodec(*cpu, cfg, 0));
   }
   const int K = ref_km.uu_len(), N = ref_km.cc_len();
   int32_t dims[KML_DIM_COUNT];

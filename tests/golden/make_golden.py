@@ -7,6 +7,7 @@ oracle/_ref/ref_harness, built by ``make -C oracle ref``):
     python tests/golden/make_golden.py --cases a,b     # regenerate the named CASES only
     python tests/golden/make_golden.py --sweep         # sweep/cfg5.npz (PEG8064 blind sweep counters)
     python tests/golden/make_golden.py --bench         # bench/*.npz (bench workload's reference counters)
+    python tests/golden/make_golden.py --bench-cases a,b   # the named BENCH_CASES only
     python tests/golden/make_golden.py --bench-large   # bench/large_oracle.json (oracle, 8 streams)
 
 What it writes (all small):
@@ -86,7 +87,17 @@ SWEEP_N = 400
 BENCH_CASES = {
     "peg2304_qpsk_known_32768": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, True, 20, 2.0, 32768, True),
     "peg2304_qpsk_blind_32768": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.0, 32768, True),
+    # cfg3: 5G BG2 + 16QAM-Gray, known channel, 50 iterations (bench_bg2 line)
+    "bg2_16qam_known_16384": ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, True, 50, 5.01, 16384, True),
+    # cfg4: PEG8064 + 64QAM-Gray, blind k-means (bench_peg8064 line); the reference runs
+    # this point at ~0.8 codewords/s on one core, so the stream is 2048 codewords
+    "peg8064_64qam_blind_2048": ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, False, 20, 6.77, 2048, True),
 }
+# cfg5: the other four sweep points (Eb/N0 0, 1, 3, 4 dB), 1024 codewords each
+for _snr in SWEEP_SNRS:
+    if _snr != 6.77:
+        BENCH_CASES[f"peg8064_64qam_blind_s{int(round(_snr * 100))}_1024"] = (
+            "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, False, 20, _snr, 1024, True)
 
 COUNTER_CASES = {
     "peg2304_qpsk_known_2000": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, True, 20, 2.0, 2000, True),
@@ -352,10 +363,13 @@ def make_sweep(tmp):
         print(f"cfg5 snr {snr}: FER {c['fer']:.4f} BER {c['ber']:.6f}")
 
 
-def make_bench(tmp):
+def make_bench(tmp, names=None):
+    """names: a subset of BENCH_CASES (--bench-cases a,b); each stream is one
+    sequential reference run, so the cases run in parallel processes."""
     from concurrent.futures import ThreadPoolExecutor
 
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
+    names = names or list(BENCH_CASES)
 
     def one(name):
         mat, mod, is5g, known, it, snr, n, active = BENCH_CASES[name]
@@ -366,9 +380,9 @@ def make_bench(tmp):
                             errs=errs.astype(np.int16))
         return f"{name}: FER {c['fer']:.5f} BER {c['ber']:.6f}"
 
-    with ThreadPoolExecutor(2) as ex:
-        for line in ex.map(one, BENCH_CASES):
-            print(line)
+    with ThreadPoolExecutor(min(len(names), 6)) as ex:
+        for line in ex.map(one, names):
+            print(line, flush=True)
 
 
 # Larger reference samples of the bench points for the Monte-Carlo BER sigma:
@@ -377,7 +391,13 @@ def make_bench(tmp):
 BENCH_LARGE = {
     "peg2304_qpsk_known": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, True, 20, 2.0, 32768),
     "peg2304_qpsk_blind": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.0, 16384),
+    # cfg3 (bench_bg2: 16384 GPU codewords per stats pass)
+    "bg2_16qam_known": ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, True, 50, 5.01, 4096),
 }
+# cfg4 / cfg5 (bench_peg8064 at 6.77 dB and the sweep points: 4096 GPU codewords per stats pass)
+for _snr in SWEEP_SNRS:
+    BENCH_LARGE["peg8064_64qam_blind" + ("" if _snr == 6.77 else f"_s{int(round(_snr * 100))}")] = (
+        "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, False, 20, _snr, 1024)
 
 
 def make_bench_large(tmp):
@@ -386,7 +406,13 @@ def make_bench_large(tmp):
         with open(os.path.join(REF_CFG, fn), "rb") as f, open(os.path.join(tmp, fn), "wb") as g:
             g.write(f.read())
     out = {}
-    for name, (mat, mod, is5g, known, it, snr, n) in BENCH_LARGE.items():
+    fn = os.path.join(HERE, "bench", "large_oracle.json")
+    names = list(BENCH_LARGE)
+    if "--only" in sys.argv:  # regenerate the named entries, keep the others
+        names = sys.argv[sys.argv.index("--only") + 1].split(",")
+        out = json.load(open(fn))
+    for name in names:
+        mat, mod, is5g, known, it, snr, n = BENCH_LARGE[name]
         r = subprocess.run([exe, os.path.join(tmp, mat), os.path.join(tmp, mod), str(int(is5g)), repr(snr), str(it),
                             str(int(not known)), str(n), "8"], check=True, capture_output=True, text=True)
         d = json.loads(r.stdout.strip().splitlines()[-1])
@@ -394,9 +420,9 @@ def make_bench_large(tmp):
                          seeds="17..24", codewords=d["codewords"], err_bit=d["err_bit"], err_blk=d["err_blk"],
                          sum_e2=d["sum_e2"], K=d["K"], ber=d["ber"], fer=d["fer"],
                          source="oracle/cpu_baseline (oracle.c restatement, bit-exact vs the reference)")
-        print(name, out[name])
+        print(name, out[name], flush=True)
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
-    with open(os.path.join(HERE, "bench", "large_oracle.json"), "w") as f:
+    with open(fn, "w") as f:
         json.dump(out, f, indent=1)
 
 
@@ -410,6 +436,13 @@ def main():
             finally:
                 shutil.rmtree(tmp)
             return
+    if "--bench-cases" in sys.argv:
+        tmp = tempfile.mkdtemp()
+        try:
+            make_bench(tmp, sys.argv[sys.argv.index("--bench-cases") + 1].split(","))
+        finally:
+            shutil.rmtree(tmp)
+        return
     if "--cases" in sys.argv:
         names = sys.argv[sys.argv.index("--cases") + 1].split(",")
         tmp = tempfile.mkdtemp()

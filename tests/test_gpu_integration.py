@@ -24,11 +24,17 @@ EXE = os.path.join(REPO, "oracle", "_ref", "shim_check")
     ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.0, 100),
     ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, True, 50, 5.01, 40),
     ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, False, 50, 5.01, 30),
+    # PEG8064 (bp_part_kernel); the reference's two codec constructions take
+    # about a minute each on one core (SystemMatrixH of 4032 x 8064)
+    pytest.param("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, True, 20, 6.77, 12,
+                 marks=pytest.mark.timeout(420)),
+    pytest.param("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, False, 20, 6.77, 6,
+                 marks=pytest.mark.timeout(420)),
 ])
 def test_reference_side_shims_match_reference_classes(data_dir, tmp_path, matrix, modem, is5g, known, max_iter, snr, n):
     cfg = str(tmp_path / "config.toml")
     write_config(cfg, data_dir, matrix, modem, is5g=is5g, known=known, max_iter=max_iter, snr=snr)
-    r = subprocess.run([EXE, cfg, repr(snr), str(n)], capture_output=True, text=True, timeout=240, cwd=tmp_path)
+    r = subprocess.run([EXE, cfg, repr(snr), str(n)], capture_output=True, text=True, timeout=400, cwd=tmp_path)
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     print(res)
