@@ -8,7 +8,7 @@ ARCH     ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result -Wno-unused-value
 CSRC     := kmldpc_amd/csrc
 OBJDIR   := build/obj
-CPP_SRCS := config code modem layout capi simulate refstream
+CPP_SRCS := config code modem layout capi simulate refstream comm
 HIP_SRCS := bp bp_regular bp_irregular bp_coop demap kmeans framegen
 OBJS     := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(CPP_SRCS) $(HIP_SRCS)))
 HDRS     := $(wildcard $(CSRC)/*.hpp) include/kmldpc_amd.h
@@ -32,7 +32,7 @@ $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -ldl -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -C oracle
@@ -54,7 +54,7 @@ $(OBJDIR)/stamps/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)/stamps
 	$(HIPCC) $(HIPFLAGS) -DKML_STAMPS=1 -c -o $@ $<
 $(STAMPS_LIB): $(STAMPS_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(STAMPS_OBJS) -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(STAMPS_OBJS) -ldl -Wl,-rpath,/opt/rocm/lib
 stamps: $(STAMPS_LIB)
 .PHONY: stamps
 
@@ -69,7 +69,7 @@ $(VAR_DIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(VAR_DIR)
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $@ $<
 kmldpc_amd/libkmldpc_amd_$(V).so: $(VAR_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(VAR_OBJS) -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(VAR_OBJS) -ldl -Wl,-rpath,/opt/rocm/lib
 variant:
 	@test -n "$(V)" || (echo "variant: set V=<name>" && false)
 	$(MAKE) kmldpc_amd/libkmldpc_amd_$(V).so V=$(V) VFLAGS='$(VFLAGS)'

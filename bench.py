@@ -324,15 +324,18 @@ def main():
     device = local
     ranks_seen = 1
     if world > 1 or args.force_dist:
-        import torch
+        # torch.distributed (gloo) is the rendezvous and CPU control channel only
+        # (barriers, the RCCL id broadcast, the timing gather).  The counters'
+        # all-reduce is the library's own RCCL communicator (kml_comm_*) on the
+        # context's stream: torch never initialises a HIP runtime of its own in
+        # this process (its bundled runtime beside the library's is two ROCm
+        # runtimes in one process, and the second to start finds no device).
         import torch.distributed as dist_mod
 
-        if args.dist_backend == "nccl":
-            torch.cuda.set_device(local)
-            dist_mod.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-        else:  # gloo: counters reduced on the CPU; ranks may share a GPU (tests on a 1-GPU box)
+        dist_mod.init_process_group(backend="gloo")
+        if args.dist_backend == "gloo":  # counters reduced on the CPU; ranks may share a GPU (tests on a 1-GPU box)
+            import torch
             device = local % max(torch.cuda.device_count(), 1)
-            dist_mod.init_process_group(backend="gloo")
         dist = dist_mod
         ranks_seen = dist.get_world_size()
 
@@ -341,6 +344,12 @@ def main():
     d = data_dir()
     cfg = write_config(d, args)
     ctx = K.Context(cfg, data_dir=d, device=device)
+    comm_ranks = 0
+    if dist is not None and args.dist_backend == "nccl":
+        uid = [K.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(uid[0], ranks_seen, rank)  # RCCL communicator over the ranks' GPUs (xGMI)
+        comm_ranks = ctx.comm_size()
     B = args.batch
     # frames for global codeword indices [rank*B, (rank+1)*B): resident in HBM
     ctx.sim_generate(args.snr, B, seed=args.seed, first_cw=rank * B)
@@ -348,9 +357,6 @@ def main():
     def barrier():
         ctx.sync()
         if dist is not None:
-            if args.dist_backend == "nccl":
-                import torch
-                torch.cuda.synchronize()
             dist.barrier()
 
     for _ in range(args.warmup):
@@ -389,13 +395,15 @@ def main():
     t_max, fl_max, per_rank = elapsed, fl_t, [elapsed]
     if dist is not None:
         import torch
-        dev = "cuda" if args.dist_backend == "nccl" else "cpu"
-        tv = torch.tensor(vals, device=dev)
-        dist.all_reduce(tv)  # RCCL over xGMI: the only collective
-        vals = tv.cpu().numpy()
-        tt = torch.tensor([elapsed, fl_t], device=dev, dtype=torch.float64)
+        if comm_ranks:
+            vals = ctx.comm_allreduce(np.ascontiguousarray(vals, np.float64))  # RCCL over xGMI: the only collective
+        else:
+            tv = torch.tensor(vals)
+            dist.all_reduce(tv)  # gloo (CPU counters)
+            vals = tv.numpy()
+        tt = torch.tensor([elapsed, fl_t], dtype=torch.float64)
         gathered = [torch.zeros_like(tt) for _ in range(ranks_seen)]
-        dist.all_gather(gathered, tt)
+        dist.all_gather(gathered, tt)  # timing: CPU control channel
         per_rank = [float(g[0].item()) for g in gathered]
         t_max = max(per_rank)
         fl_max = max(float(g[1].item()) for g in gathered)
@@ -508,9 +516,9 @@ def main():
             "global_batch": B * world,
             "parallelism": f"codeword-sharded x{world}",
         },
-        "dist_backend": args.dist_backend if dist is not None else None,
-        # ranks of the RCCL process group (0: no process group, or gloo)
-        "rccl_ranks": ranks_seen if (dist is not None and args.dist_backend == "nccl") else 0,
+        "dist_backend": (("rccl" if comm_ranks else "gloo") + " counters, gloo control") if dist is not None else None,
+        # ranks of the library's RCCL communicator (0: none — one process, or gloo counters)
+        "rccl_ranks": comm_ranks,
         "ranks": ranks_seen,
         "rank_ms_per_step": [round(t / args.steps * 1e3, 3) for t in per_rank],
         "full_loop": {

@@ -172,7 +172,9 @@ int kml_count_errors(kml_ctx *ctx, const uint8_t *uu, const uint8_t *uu_hat, int
 int kml_sim_generate(kml_ctx *ctx, double snr, uint64_t seed, uint64_t first_cw, int B);
 /* Receive the resident batch (blind or known-H) and accumulate the counters.
  * counters[8] (may be NULL) receives {err_bit, err_blk, tot_bit, tot_blk,
- * vn_phases, cn_phases, converged, 0} of this call.  If sync == 0 the call
+ * vn_phases, cn_phases, converged, redone} of this call (redone: codewords whose
+ * fast decode met a quotient it could not prove correctly rounded and was
+ * decoded again on the exact path; see DESIGN.md "Exact division").  If sync == 0 the call
  * returns after enqueueing the work (counters must then be NULL); use
  * kml_sync to wait. */
 int kml_sim_decode(kml_ctx *ctx, double snr, int blind, uint64_t *counters, int sync);
@@ -238,6 +240,23 @@ int kml_sim_load(kml_ctx *ctx, double snr, const uint8_t *uu, const double *y, c
 /* Copy the resident frames out (for checks): uu[B][K] bytes, y[B][S][2], h[B][2]. */
 int kml_sim_frames(kml_ctx *ctx, uint8_t *uu, double *y, double *h);
 
+/* --- multi-GPU counter reduction: RCCL over xGMI ------------------------- */
+/* The reference sums its worker threads' counters under a mutex
+ * (lib/lab/src/threadsafe_sourcesink.cc); across GPUs that is one RCCL
+ * all-reduce, issued by this library on the context's stream.  Rank 0 calls
+ * kml_comm_unique_id, the caller distributes the 128 bytes (any CPU channel,
+ * e.g. torch.distributed gloo), and every rank calls kml_comm_init (a
+ * collective).  librccl.so.1 is loaded on first use. */
+#define KML_COMM_ID_BYTES 128
+int kml_comm_unique_id(uint8_t *id /* [KML_COMM_ID_BYTES] */);
+int kml_comm_init(kml_ctx *ctx, const uint8_t *id, int world, int rank);
+/* Ranks of the context's communicator (0 = none). */
+int kml_comm_size(const kml_ctx *ctx);
+/* In-place sum over the ranks of n host values (staged through the GPU;
+ * synchronous). */
+int kml_comm_allreduce_u64(kml_ctx *ctx, uint64_t *vals, int n);
+int kml_comm_allreduce_f64(kml_ctx *ctx, double *vals, int n);
+
 /* --- the reference's host random sources (parity runs) ------------------ */
 /* lab::CLCRandNum (randnum.cc:4-92): Park-Miller minimal standard with
  * Schrage's method; *state = 17 is SetSeed(-1).  Normal(): polar method. */
@@ -272,10 +291,13 @@ int kml_prof_read_flops(kml_ctx *ctx, const char *stage, double *alg_flops);
 int kml_math_probe(kml_ctx *ctx, const double *in, int n, double *out);
 /* Device-side probe of the soft metric's log (kml_log, glibc-exact): out[i] = log(in[i]). */
 int kml_log_probe(kml_ctx *ctx, const double *in, int n, double *out);
-/* Device-side probe of the decoder's shared-reciprocal division: in[n][3] =
- * (n0, n1, s) -> out[n][8] = (fast n0/s, fast n1/s, IEEE n0/s, IEEE n1/s,
- * CN-phase n0/s, CN-phase n1/s (near-one reciprocal), the near-one reciprocal
- * formula of s, hipcc's refined reciprocal of s) — see bp_common.hpp. */
+/* Device-side probe of the decoder's divisions (exact_div.hpp, bp_common.hpp):
+ * in[n][3] = (n0, n1, s) -> out[n][11] = (FAST VN quotients n0/s, n1/s
+ * (dd_quot), div_rn n0/s, n1/s (correctly rounded, any operands), the CN
+ * phase's near-one quotients n0/s, n1/s, the near-one reciprocal formula of s,
+ * hipcc's refined reciprocal of s, hipcc's '/' n0/s, n1/s, flags: bit 0 / 1 =
+ * dd_check could not prove the FAST quotient of n0 / n1, bit 2 = div2's
+ * suspect flag). */
 int kml_div_probe(kml_ctx *ctx, const double *in, int n, double *out);
 /* Test hook: after the nth (0-based) cooperative BP launch from now, set that
  * kernel's abort word as a timed-out group barrier would (nth < 0: off).  The

@@ -33,6 +33,15 @@ KML_HISTOGRAM = 2
 DIM_NAMES = ["M", "Ncol", "K", "cc_len", "Z", "E", "chk", "max_iter", "bits", "Kc", "S", "bp_lds"]
 
 
+def comm_unique_id():
+    """A fresh RCCL unique id (128 bytes) for kml_comm_init (rank 0 calls it)."""
+    u = np.zeros(128, np.uint8)
+    r = lib().kml_comm_unique_id(_p(u))
+    if r != 0:
+        raise KmlError(f"kml_comm_unique_id failed (code {r}): librccl.so.1 not loadable?")
+    return u.tobytes()
+
+
 class KmlError(RuntimeError):
     pass
 
@@ -96,6 +105,11 @@ def lib():
         "kml_math_probe": (I, [P, P, I, P]),
         "kml_div_probe": (I, [P, P, I, P]),
         "kml_debug_inject_abort": (I, [P, I]),
+        "kml_comm_unique_id": (I, [P]),
+        "kml_comm_init": (I, [P, P, I, I]),
+        "kml_comm_size": (I, [P]),
+        "kml_comm_allreduce_u64": (I, [P, P, I]),
+        "kml_comm_allreduce_f64": (I, [P, P, I]),
         "kml_log_probe": (I, [P, P, I, P]),
         "kml_lcg_uniform": (D, [P]),
         "kml_lcg_normal": (None, [P, P, I]),
@@ -109,7 +123,10 @@ def lib():
         "kml_sweep_point": (I, [C.POINTER(PointCfg), BATCH_FN, P, ALLREDUCE_FN, P, REPORT_FN, P, P]),
         "kml_sim_point": (I, [P, C.POINTER(PointCfg), C.c_uint64, ALLREDUCE_FN, P, REPORT_FN, P, P]),
     }
+    ab_build = "KML_LIB" in os.environ  # an A/B build of other sources may predate newer entry points
     for name, (res, args) in sig.items():
+        if ab_build and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -301,8 +318,8 @@ class Context:
             return None
         cnt = np.zeros(8, np.uint64)
         self._chk(lib().kml_sim_decode(self._h, float(snr), int(blind), _p(cnt), 1), "kml_sim_decode")
-        return dict(zip(["err_bit", "err_blk", "tot_bit", "tot_blk", "vn_phases", "cn_phases", "converged"],
-                        [int(x) for x in cnt[:7]]))
+        return dict(zip(["err_bit", "err_blk", "tot_bit", "tot_blk", "vn_phases", "cn_phases", "converged", "redone"],
+                        [int(x) for x in cnt[:8]]))
 
     def bp_kernel(self):
         """Name of the BP kernel family the last decode launched."""
@@ -320,7 +337,7 @@ class Context:
         self._chk(lib().kml_sim_decode_ex(self._h, float(snr), int(blind), int(histogram), _p(err), _p(met), _p(cnt)),
                   "kml_sim_decode_ex")
         return err, met, dict(zip(["err_bit", "err_blk", "tot_bit", "tot_blk", "vn_phases", "cn_phases",
-                                   "converged"], [int(x) for x in cnt[:7]]))
+                                   "converged", "redone"], [int(x) for x in cnt[:8]]))
 
     def run_config(self):
         """The parsed config.toml ([range], [decoder], [xcodec], [histogram], [ldpc])."""
@@ -374,9 +391,31 @@ class Context:
 
     def div_probe(self, x):
         x = _f64(x).reshape(-1, 3)
-        out = np.zeros((x.shape[0], 8))
+        out = np.zeros((x.shape[0], 11))
         self._chk(lib().kml_div_probe(self._h, _p(x), x.shape[0], _p(out)), "kml_div_probe")
         return out
+
+    # ---- multi-GPU counter reduction (RCCL over xGMI, kml_comm_*)
+    def comm_init(self, uid, world, rank):
+        """Join the RCCL communicator of `world` ranks (a collective); uid from
+        comm_unique_id() on rank 0, distributed over any CPU channel."""
+        u = np.frombuffer(bytes(uid), np.uint8).copy()
+        if u.size != 128:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        self._chk(lib().kml_comm_init(self._h, _p(u), int(world), int(rank)), "kml_comm_init")
+
+    def comm_size(self):
+        return int(lib().kml_comm_size(self._h))
+
+    def comm_allreduce(self, vals):
+        """In-place sum over the ranks of a uint64 or float64 numpy array (RCCL)."""
+        if vals.dtype == np.uint64:
+            self._chk(lib().kml_comm_allreduce_u64(self._h, _p(vals), vals.size), "kml_comm_allreduce_u64")
+        elif vals.dtype == np.float64:
+            self._chk(lib().kml_comm_allreduce_f64(self._h, _p(vals), vals.size), "kml_comm_allreduce_f64")
+        else:
+            raise TypeError("comm_allreduce: uint64 or float64")
+        return vals
 
     def debug_inject_abort(self, nth):
         """Test hook: raise the abort word after the nth cooperative BP launch."""

@@ -111,8 +111,8 @@ __global__ __launch_bounds__(T) void bp_kernel(DevCode c, BpLaunch a, unsigned i
             const double n0 = a0 * c0;
             const double n1 = a1 * (1.0 - c0);
             const double s = n0 + n1;
-            a0 = n0 / s;
-            a1 = n1 / s;
+            a0 = div_rn(n0, s);
+            a1 = div_rn(n1, s);
           }
         }
         cch[v] = (a0 > a1) ? 0 : 1;  // :190-194
@@ -123,14 +123,14 @@ __global__ __launch_bounds__(T) void bp_kernel(DevCode c, BpLaunch a, unsigned i
             const double t0 = al0[k] * b0;
             const double t1 = al1[k] * b1;
             const double s = t0 + t1;
-            slots[es[k]] = make_double2(t0 / s, t1 / s);
+            slots[es[k]] = make_double2(div_rn(t0, s), div_rn(t1, s));
             if (k > 0) {  // the head's beta (k == 0) is dead
               const double c0 = c0s[k];
               const double n0 = b0 * c0;
               const double n1 = b1 * (1.0 - c0);
               const double s2 = n0 + n1;
-              b0 = n0 / s2;
-              b1 = n1 / s2;
+              b0 = div_rn(n0, s2);
+              b1 = div_rn(n1, s2);
             }
           }
         }
@@ -169,8 +169,8 @@ __global__ __launch_bounds__(T) void bp_kernel(DevCode c, BpLaunch a, unsigned i
               const double n0 = a0 * m.x + a1 * m.y;
               const double n1 = a0 * m.y + a1 * m.x;
               const double s = n0 + n1;
-              a0 = n0 / s;
-              a1 = n1 / s;
+              a0 = div_rn(n0, s);
+              a1 = div_rn(n1, s);
             }
           }
         }
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(T) void bp_kernel(DevCode c, BpLaunch a, unsigned i
             const double t0 = al0[k] * b0 + al1[k] * b1;
             const double t1 = al0[k] * b1 + al1[k] * b0;
             const double s = t0 + t1;
-            double q = t0 / s;  // t1/s is dead (:259 overwritten at :264)
+            double q = div_rn(t0, s);  // t1/s is dead (:259 overwritten at :264)
             if (q > 1.0 - kSmallestProb) q = 1.0 - kSmallestProb;
             if (q < kSmallestProb) q = kSmallestProb;
             slots[b + k].x = q;
@@ -189,8 +189,8 @@ __global__ __launch_bounds__(T) void bp_kernel(DevCode c, BpLaunch a, unsigned i
               const double n0 = b0 * v0[k] + b1 * v1[k];
               const double n1 = b0 * v1[k] + b1 * v0[k];
               const double s2 = n0 + n1;
-              b0 = n0 / s2;
-              b1 = n1 / s2;
+              b0 = div_rn(n0, s2);
+              b1 = div_rn(n1, s2);
             }
           }
         }
@@ -358,6 +358,16 @@ hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const c
   if (family) *family = "bp_kernel";
   if (lds) return syn ? dispatch_deg<true, true>(c, a, queue, s, err) : dispatch_deg<true, false>(c, a, queue, s, err);
   return syn ? dispatch_deg<false, true>(c, a, queue, s, err) : dispatch_deg<false, false>(c, a, queue, s, err);
+}
+
+int bp_fast_mode(const DevCode &c) {
+  if (c.dv_max > kFastMaxColumnDegree) return 0;
+  if (const char *e = getenv("KML_NO_FAST"))
+    if (e[0] == '1') return 0;
+  int m = 1;
+  if (const char *e = getenv("KML_FORCE_REDO"))
+    if (e[0] == '1') m |= 2;
+  return m;
 }
 
 }  // namespace kml

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "exact_div.hpp"
+
 namespace kml {
 
 constexpr double kSmallestProb = 1.0e-12;  // lib/lab/include/utility.h:12
@@ -47,28 +49,30 @@ __device__ __forceinline__ int wg_any(int pred, int *wflags) {
   return r;
 }
 
+// Two workgroup ORs with one barrier (same rules as wg_any): bit 0 = OR of
+// p0, bit 1 = OR of p1.
+template <int NW>
+__device__ __forceinline__ int wg_any2(int p0, int p1, int *wflags) {
+  static_assert(NW % 4 == 0 && NW <= 16, "wave flags are read as int4");
+  const int any = (__ballot(p0) != 0 ? 1 : 0) | (__ballot(p1) != 0 ? 2 : 0);
+  if ((threadIdx.x & 63) == 0) wflags[threadIdx.x >> 6] = any;
+  __syncthreads();
+  int r = 0;
+#pragma unroll
+  for (int w = 0; w < NW; w += 4) {
+    const int4 v = *reinterpret_cast<const int4 *>(wflags + w);
+    r |= v.x | v.y | v.z | v.w;
+  }
+  return r;
+}
+
 template <int NW>
 __device__ __forceinline__ int wg_all(int pred, int *wflags) {
   return !wg_any<NW>(!pred, wflags);
 }
 
-// q0 = n0 / s and q1 = n1 / s, both correctly rounded.
-//
-// FAST = false: two IEEE divisions.
-// FAST = true : one shared reciprocal refinement and two residual corrections —
-// exactly the instruction sequence hipcc emits for an f64 '/' on gfx950
-// (v_div_scale, v_rcp_f64, 2 Newton steps, v_mul, residual fma, v_div_fmas,
-// v_div_fixup) with the scale / fixup steps dropped.  Those steps are identity
-// operations unless an operand or the quotient is outside the normal range
-// (denominator or quotient denormal, numerator < 2^-969, exponent gap >= 768,
-// zero / inf / NaN denominators).  The caller guarantees that: it takes the FAST
-// path only for codewords whose priors are 0, 1 or in [2^-40, 1-2^-40] on codes
-// with column degree <= 20, which bounds every nonzero message, sum and quotient
-// of the decoder below 1 and above 2^-840 ("Exact fast division").
 // hipcc's reciprocal refinement of an f64 '/': v_rcp_f64 and two Newton steps.
-// (-r) * s + 1 is the same exact product-sum as (-s) * r + 1; negating the
-// per-use operand lets the negation ride on an fma source modifier instead of
-// a materialised -s shared across branches (two VALU moves per sum).
+// Used only by the div probe (tests) to show where it is not RN(1/s).
 __device__ __forceinline__ double rcp_refine(double s) {
   double r = __builtin_amdgcn_rcp(s);
   double e = fma(-r, s, 1.0);
@@ -144,39 +148,56 @@ __device__ __forceinline__ double qdiv_r(double n, double s, double r) {
 
 // One CN step's normalisations for R rows: the c2v quotients clip(t0 / ts)
 // and the chain states (n0, n1) / (n0 + n1) (binaryldpccodec.cc:241-266), the
-// sums' reciprocals from rcp_cn_rows on the FAST path, IEEE divisions else.
+// sums' reciprocals from rcp_cn_rows on the FAST path, div_rn else.
 template <int R, bool FAST>
 __device__ __forceinline__ void cn_c2v_rows(const double (&t0)[R], const double (&ts)[R], double (&q)[R]);
 template <int R, bool FAST>
 __device__ __forceinline__ void cn_norm_rows(const double (&n0)[R], const double (&n1)[R], double (&s0)[R],
                                              double (&s1)[R]);
 
+// q0 = RN(n0 / s) and q1 = RN(n1 / s) (binaryldpccodec.cc:177-273 divide
+// with x86 divsd).
+//   FAST, CN: s within 2^-49 of 1 (every CN-phase sum and the VN phase's
+//     unit-beta step): the near-one reciprocal and the division tail, exact by
+//     exhaustive enumeration (rcp_near1).
+//   FAST, VN: exact_div.hpp dd_quot — faithful always, and proven correctly
+//     rounded by dd_check; a quotient the check cannot prove sets sus, and the
+//     caller redoes the codeword on the exact path (FAST = false).  The FAST
+//     path runs only for codewords whose priors are 0, 1 or in
+//     [2^-40, 1-2^-40] on codes with column degree <= 20, which keeps every
+//     nonzero message, sum and quotient in [2^-840, 2] ("Exact
+//     division"), inside dd_check's domain.
+//   !FAST: div_rn (any operands).
 template <bool FAST, bool CN = false>
-__device__ __forceinline__ void div2(double n0, double n1, double s, double &q0, double &q1) {
+__device__ __forceinline__ void div2(double n0, double n1, double s, double &q0, double &q1, bool &sus) {
   if constexpr (!FAST) {
-    q0 = n0 / s;
-    q1 = n1 / s;
+    q0 = div_rn(n0, s);
+    q1 = div_rn(n1, s);
+  } else if constexpr (CN) {
+    const double r = rcp_cn(s);
+    q0 = qdiv_r(n0, s, r);
+    q1 = qdiv_r(n1, s, r);
   } else {
-    const double r = CN ? rcp_cn(s) : rcp_refine(s);
-    const double m0 = n0 * r;
-    const double m1 = n1 * r;
-    const double f0 = fma(-m0, s, n0);
-    const double f1 = fma(-m1, s, n1);
-    q0 = fma(f0, r, m0);
-    q1 = fma(f1, r, m1);
+    const DdRcp y = dd_rcp(s);
+    q0 = dd_quot(n0, y);
+    q1 = dd_quot(n1, y);
+    sus |= !((int)dd_check(n0, s, q0, y) & (int)dd_check(n1, s, q1, y));
   }
 }
+// the CN phase's form (near-one sums: nothing to prove at run time)
+template <bool FAST, bool CN>
+__device__ __forceinline__ void div2(double n0, double n1, double s, double &q0, double &q1) {
+  static_assert(CN, "VN divisions carry a suspect flag");
+  bool unused = false;
+  div2<FAST, CN>(n0, n1, s, q0, q1, unused);
+}
 
-template <bool FAST, bool CN = false>
+// n0 / s for the CN phase (near-one sums on the FAST path)
+template <bool FAST, bool CN = true>
 __device__ __forceinline__ double div1(double n0, double s) {
-  if constexpr (!FAST) {
-    return n0 / s;
-  } else {
-    const double r = CN ? rcp_cn(s) : rcp_refine(s);
-    const double m0 = n0 * r;
-    const double f0 = fma(-m0, s, n0);
-    return fma(f0, r, m0);
-  }
+  static_assert(CN, "div1 is the CN phase's division");
+  if constexpr (!FAST) return div_rn(n0, s);
+  else return qdiv_r(n0, s, rcp_cn(s));
 }
 
 // The first backward step of a column multiplies beta = (1, 1) by the c2v pair
@@ -219,7 +240,7 @@ __device__ __forceinline__ void cn_c2v_rows(const double (&t0)[R], const double 
     for (int i = 0; i < R; ++i) q[i] = clip_c2v<true>(qdiv_r(t0[i], ts[i], rc[i]));
   } else {
 #pragma unroll
-    for (int i = 0; i < R; ++i) q[i] = clip_c2v<false>(t0[i] / ts[i]);
+    for (int i = 0; i < R; ++i) q[i] = clip_c2v<false>(div_rn(t0[i], ts[i]));
   }
 }
 template <int R, bool FAST>
@@ -239,8 +260,8 @@ __device__ __forceinline__ void cn_norm_rows(const double (&n0)[R], const double
   } else {
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      s0[i] = n0[i] / ns[i];
-      s1[i] = n1[i] / ns[i];
+      s0[i] = div_rn(n0[i], ns[i]);
+      s1[i] = div_rn(n1[i], ns[i]);
     }
   }
 }
@@ -252,14 +273,14 @@ __device__ __forceinline__ void cn_norm_rows(const double (&n0)[R], const double
 // the gap exceeds an ulp); only then is the division skipped (FAST path, all
 // values finite and >= +0).
 template <bool FAST>
-__device__ __forceinline__ int hard_decision(double n0, double n1) {
+__device__ __forceinline__ int hard_decision(double n0, double n1, bool &sus) {
   if constexpr (FAST) {
     const double g = 1.0 + 0x1p-48;
     if (n0 > n1 * g) return 0;
     if (n1 > n0 * g) return 1;
   }
   double a0, a1;
-  div2<FAST>(n0, n1, n0 + n1, a0, a1);
+  div2<FAST>(n0, n1, n0 + n1, a0, a1, sus);
   return (a0 > a1) ? 0 : 1;
 }
 

@@ -46,7 +46,7 @@ namespace {
 
 struct GroupSync {
   unsigned bar;      // barrier arrivals (monotonic within a launch)
-  unsigned flag[2];  // parity-failure flags, alternating per iteration
+  unsigned flag[2];  // per iteration parity: bit 0 failing rows, bit 1 an unproven VN quotient
   unsigned cw;       // the group's current codeword (entry index)
   unsigned nofast;   // some member saw a prior outside the FAST division domain
   unsigned errs;     // error bits of the codeword, summed over members
@@ -56,7 +56,8 @@ struct GroupSync {
   // low 32 bits, parity-failure reports in the high 32 bits (part_barrier)
   unsigned long long bar2[2];
   // tagged exchange: early-stop flags per iteration parity and member,
-  // ((global iteration + 1) << 1) | (the member has failing rows)
+  // ((global iteration + 1) << 2) | (an unproven quotient in its VN phase) << 1
+  // | (the member has failing rows)
   unsigned long long mflag[2][4];
 };
 
@@ -145,17 +146,20 @@ struct CoopCtl {
   unsigned abort;  // a group barrier timed out: every workgroup exits
 };
 
+// Returns -1 when the launch aborts, 1 when a FAST decode met a quotient
+// dd_check could not prove (exact_div.hpp; the caller redoes the codeword with
+// FAST = false), 0 when done.
 template <int kG, int RV, int RC, bool SYN, bool FAST>
-__device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch &a, int cw, GroupSync *gs,
+__device__ __forceinline__ int coop_iterations(const DevCode &c, const BpLaunch &a, int cw, GroupSync *gs,
                                                 unsigned &gen, bool same_xcd, unsigned *abort, double2 *slots,
                                                 uint8_t *gc, const int (&vpos)[RV], const int (&es)[RV][3],
                                                 const bool (&vact)[RV], const double (&pv)[RV], const int (&crow)[RC],
                                                 const int (&cbase)[RC], const int (&ccol)[RC][3],
                                                 const bool (&cact)[RC], int odd, int member, int &iter_out,
-                                                bool &conv_out) {
+                                                bool &conv_out, bool sus0 = false) {
   constexpr int DV = 3, DC = 6, H = 3;
   int iter = 0;
-  bool conv = false;
+  bool conv = false, sus = sus0;
   for (; iter < a.iter_count; ++iter) {
     // ------------------------------------------------------------ VN phase
     // falling wave priorities within a phase (see bp_regular.hip)
@@ -182,9 +186,9 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
           const double n0 = a0[r] * c0;
           const double n1 = a1[r] * (1.0 - c0);
           if (k + 1 < DV) {
-            div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r]);
+            div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r], sus);
           } else {
-            const int hd = hard_decision<FAST>(n0, n1);
+            const int hd = hard_decision<FAST>(n0, n1, sus);
             if (vact[r]) gc[vpos[r]] = (unsigned char)hd;
           }
         }
@@ -203,9 +207,9 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
           const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
           double q0, q1;
           if (unit)  // beta = (1, 1): t is the normalised alpha, its sum within ulps of 1 (bp_common.hpp rcp_near1)
-            div2<FAST, true>(t0, t1, t0 + t1, q0, q1);
+            div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
           else
-            div2<FAST>(t0, t1, t0 + t1, q0, q1);
+            div2<FAST>(t0, t1, t0 + t1, q0, q1, sus);
           if (vact[r]) slots[es[r][k]] = make_double2(q0, q1);
           if (k > 0) {
             const double c0 = c0s[r][k];
@@ -213,13 +217,13 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
               b0[r] = c0;
               b1[r] = 1.0 - c0;
             } else {
-              div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r]);
+              div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r], sus);
             }
           }
         }
       }
     }
-    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return false;
+    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return -1;
 
     // -------------------- early-stop parity check, folded into the CN barrier
     // Every member ORs its failing-row flag now and runs the CN phase
@@ -235,8 +239,9 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
         for (int k = 0; k < H; ++k) p ^= ld_nt(&gc[ccol[r][k]]);
         fail |= cact[r] ? (p ^ swap_pair_i(p)) : 0;
       }
-      if (__ballot(fail) != 0 && (threadIdx.x & 63) == 0)
-        __hip_atomic_fetch_or(&gs->flag[iter & 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned bits = (__ballot(fail) != 0 ? 1u : 0u) | (__ballot(sus) != 0 ? 2u : 0u);
+      if (bits && (threadIdx.x & 63) == 0)
+        __hip_atomic_fetch_or(&gs->flag[iter & 1], bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     // ------------------------------------------------------------ CN phase
@@ -290,7 +295,7 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
             const bool unit = FAST && st == 0;
             const double n0 = unit ? m0[r] : s0[r] * m0[r] + s1[r] * m1[r];
             const double n1 = unit ? m1[r] : s0[r] * m1[r] + s1[r] * m0[r];
-            div2<FAST, true>(n0, n1, n0 + n1, s0[r], s1[r]);
+            div2<FAST, true>(n0, n1, n0 + n1, s0[r], s1[r], sus);
           }
         }
         if (st >= H) {
@@ -302,8 +307,14 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
 #pragma unroll
       for (int r = 0; r < RC; ++r) syn0[r] = s0[r];
     }
-    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return false;
-    if (!ld_rlx(&gs->flag[iter & 1])) {  // every row satisfied: stop before this CN phase
+    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return -1;
+    const unsigned fl = ld_rlx(&gs->flag[iter & 1]);
+    if (FAST && (fl & 2u)) {  // an unproven quotient in this VN phase (every member reads the same word)
+      iter_out = iter;
+      conv_out = false;
+      return 1;
+    }
+    if (!(fl & 1u)) {  // every row satisfied: stop before this CN phase
       conv = true;
       break;
     }
@@ -317,10 +328,12 @@ __device__ __forceinline__ bool coop_iterations(const DevCode &c, const BpLaunch
   }
   iter_out = iter;
   conv_out = conv;
-  return true;
+  return 0;
 }
 
-template <int kG, int T, int RV, int RC, bool SYN>
+// EXACT = false: the FAST kernel (defers non-FAST and suspect codewords to
+// a.defer_idx); EXACT = true: the exact path over a defer list (bp_regular.hip).
+template <int kG, int T, int RV, int RC, bool SYN, bool EXACT>
 __global__ __launch_bounds__(T) void bp_coop_kernel(DevCode c, BpLaunch a, GroupSync *gsync, uint8_t *gcch,
                                                     unsigned *abort, unsigned int *queue, int fast_allowed) {
   const int tid = threadIdx.x;
@@ -361,6 +374,8 @@ __global__ __launch_bounds__(T) void bp_coop_kernel(DevCode c, BpLaunch a, Group
 
   // do the group's members share an XCD (one L2)?  HW_REG_XCC_ID, bits [3:0]
   unsigned gen = 0;
+  if (a.B_dev && *a.B_dev == 0) return;  // an empty defer list: every workgroup leaves before the first barrier
+  const int B = a.B_dev ? (int)*a.B_dev : a.B;
   if (tid == 0) {
     const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
     __hip_atomic_fetch_or(&gs->xcc, 1u << xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -379,7 +394,7 @@ __global__ __launch_bounds__(T) void bp_coop_kernel(DevCode c, BpLaunch a, Group
     }
     if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return;
     const int entry = (int)ld_rlx(&gs->cw);
-    if (entry >= a.B) break;
+    if (entry >= B) break;
     const int cw = a.cw_idx ? a.cw_idx[entry] : entry;
     const double *p0 = a.p0 + (long long)cw * a.p0_stride;
     if (a.p0_sel) p0 += (long long)a.p0_sel[cw] * a.p0_sel_stride;
@@ -399,18 +414,29 @@ __global__ __launch_bounds__(T) void bp_coop_kernel(DevCode c, BpLaunch a, Group
     if (__ballot(!ok) != 0 && (tid & 63) == 0)
       __hip_atomic_fetch_or(&gs->nofast, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return;
-    const bool fast = fast_allowed && !ld_rlx(&gs->nofast);
+    const bool fast = (fast_allowed & 1) && !ld_rlx(&gs->nofast);
 
     int iter = 0;
     bool conv = false;
-    bool alive;
-    if (fast)
-      alive = coop_iterations<kG, RV, RC, SYN, true>(c, a, cw, gs, gen, same_xcd, abort, slots, gc, vpos, es, vact,
-                                                     pv, crow, cbase, ccol, cact, odd, member, iter, conv);
-    else
-      alive = coop_iterations<kG, RV, RC, SYN, false>(c, a, cw, gs, gen, same_xcd, abort, slots, gc, vpos, es, vact,
-                                                      pv, crow, cbase, ccol, cact, odd, member, iter, conv);
-    if (!alive) return;
+    if constexpr (!EXACT) {
+      int st = 1;  // 1: to the exact kernel
+      if (fast)
+        st = coop_iterations<kG, RV, RC, SYN, true>(c, a, cw, gs, gen, same_xcd, abort, slots, gc, vpos, es, vact, pv,
+                                                    crow, cbase, ccol, cact, odd, member, iter, conv,
+                                                    (fast_allowed & 2) != 0);
+      if (st < 0) return;
+      if (st == 1) {  // every member took this branch (the flag word / nofast are group-wide)
+        if (member == 0 && tid == 0) {
+          a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = cw;
+          if (fast && a.counters) atomicAdd(&a.counters[CNT_REDONE], 1ull);
+        }
+        continue;
+      }
+    } else {
+      if (coop_iterations<kG, RV, RC, SYN, false>(c, a, cw, gs, gen, same_xcd, abort, slots, gc, vpos, es, vact, pv,
+                                                  crow, cbase, ccol, cact, odd, member, iter, conv) < 0)
+        return;
+    }
 
     // ---- outputs: every member writes its share; member 0 the scalars
     if (a.iter_count > 0) {
@@ -519,8 +545,8 @@ __device__ __forceinline__ int part_barrier(GroupSync *gs, unsigned long long *s
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     unsigned long long add = 1;
-    if (flag) {
-      if (*flag) add += 1ull << 32;
+    if (flag) {  // bit 0: failing rows (counts 1), bit 1: an unproven quotient (counts 256)
+      add += (unsigned long long)(((*flag & 1) ? 1u : 0u) + ((*flag & 2) ? 256u : 0u)) << 32;
       *flag = 0;  // the next reports follow this barrier
     }
     st[p] += kG;
@@ -570,8 +596,10 @@ __device__ __forceinline__ int part_barrier(GroupSync *gs, unsigned long long *s
 // by the L2 request rate; here the exchange moves ~24 bytes per cut edge per
 // iteration in mostly contiguous runs.
 
+// -1: the launch aborts; 1: a FAST decode met an unproven quotient (redo with
+// FAST = false, see coop_iterations); 0: done.
 template <int kG, int RV, int RC, int RX, bool SYN, bool FAST>
-__device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N, int NG, int cw, GroupSync *gs,
+__device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, int NG, int cw, GroupSync *gs,
                                                 unsigned long long *bst, unsigned &nb, int *sfail, bool same_xcd,
                                                 unsigned *abort, unsigned char *smem,
                                                 uint8_t *dec, double2 *mb_v2c, double *mb_c2v, uint8_t *gc,
@@ -579,7 +607,8 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
                                                 const bool (&vact)[RV], const double (&pv)[RV], const int (&crow)[RC],
                                                 const int (&cbase)[RC],
                                                 const bool (&cact)[RC], const int (&xr)[RX], const int (&xc)[RX],
-                                                int odd, int member, int &iter_out, bool &conv_out) {
+                                                int odd, int member, int &iter_out, bool &conv_out,
+                                                bool sus0 = false) {
   constexpr int DV = 3, DC = 6, H = 3;
   const int tid = threadIdx.x;
   int ccol[RC][H];  // parity-check columns (positions in dec): even lane edges [0, H), odd lane [H, DC)
@@ -589,7 +618,7 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
     for (int k = 0; k < H; ++k) ccol[r][k] = c.pt_pos[c.row_col[c.row_ptr[crow[r]] + (odd ? H + k : k)]];
   double2 *slots = reinterpret_cast<double2 *>(smem);
   int iter = 0;
-  bool conv = false;
+  bool conv = false, sus = sus0;
 #ifdef KML_STAMPS
   unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
 #endif
@@ -627,9 +656,9 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
           const double n0 = a0[r] * c0;
           const double n1 = a1[r] * (1.0 - c0);
           if (k + 1 < DV) {
-            div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r]);
+            div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r], sus);
           } else {
-            const int hd = hard_decision<FAST>(n0, n1);
+            const int hd = hard_decision<FAST>(n0, n1, sus);
             if (vact[r]) {
               dec[vpos[r]] = (unsigned char)hd;
               gc[vpos[r]] = (unsigned char)hd;
@@ -651,9 +680,9 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
           const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
           double q0, q1;
           if (unit)  // beta = (1, 1): t is the normalised alpha, its sum within ulps of 1 (bp_common.hpp rcp_near1)
-            div2<FAST, true>(t0, t1, t0 + t1, q0, q1);
+            div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
           else
-            div2<FAST>(t0, t1, t0 + t1, q0, q1);
+            div2<FAST>(t0, t1, t0 + t1, q0, q1, sus);
           if (vact[r]) *reinterpret_cast<double2 *>(smem + (vaddr[r][k] & 0xFFFF) * 16) = make_double2(q0, q1);
           if (k > 0) {
             const double c0 = c0s[r][k];
@@ -661,7 +690,7 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
               b0[r] = c0;
               b1[r] = 1.0 - c0;
             } else {
-              div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r]);
+              div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r], sus);
             }
           }
         }
@@ -674,7 +703,7 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
 #pragma unroll
     for (int q = 0; q < RX; ++q)
       if (xc[q] >= 0) mb_v2c[xc[q] >> 16] = slots[xc[q] & 0xFFFF];
-    if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return false;
+    if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return -1;
     KML_STAMP(4);  // send v2c + group barrier
 
     // ------------------- receive v2c and the other members' hard decisions
@@ -701,7 +730,8 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
         for (int k = 0; k < H; ++k) p ^= dec[ccol[r][k]];
         fail |= cact[r] ? (p ^ swap_pair_i(p)) : 0;
       }
-      if (__ballot(fail) != 0 && (tid & 63) == 0) atomicOr(sfail, 1);  // reported at the CN barrier
+      const int bits = (__ballot(fail) != 0 ? 1 : 0) | (__ballot(sus) != 0 ? 2 : 0);
+      if (bits && (tid & 63) == 0) atomicOr(sfail, bits);  // reported at the CN barrier
     }
 
     // ------------------------------------------------------------ CN phase
@@ -752,7 +782,7 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
             const bool unit = FAST && st == 0;
             const double n0 = unit ? m0[r] : s0[r] * m0[r] + s1[r] * m1[r];
             const double n1 = unit ? m1[r] : s0[r] * m1[r] + s1[r] * m0[r];
-            div2<FAST, true>(n0, n1, n0 + n1, s0[r], s1[r]);
+            div2<FAST, true>(n0, n1, n0 + n1, s0[r], s1[r], sus);
           }
         }
       }
@@ -768,8 +798,13 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
       if (xr[q] >= 0) mb_c2v[xr[q] >> 16] = slots[xr[q] & 0xFFFF].x;
     const int failing = part_barrier<kG>(gs, bst, nb, same_xcd, abort, sfail);
     KML_STAMP(8);  // send c2v + group barrier
-    if (failing < 0) return false;
-    if (failing == 0) {  // every row satisfied: stop before this CN phase
+    if (failing < 0) return -1;
+    if (FAST && (failing >> 8)) {  // a member met an unproven quotient in this VN phase
+      iter_out = iter;
+      conv_out = false;
+      return 1;
+    }
+    if ((failing & 0xFF) == 0) {  // every row satisfied: stop before this CN phase
       conv = true;
       break;
     }
@@ -781,7 +816,7 @@ __device__ __forceinline__ bool part_iterations(const BpLaunch &a, int M, int N,
   }
   iter_out = iter;
   conv_out = conv;
-  return true;
+  return 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -922,20 +957,25 @@ __device__ __forceinline__ bool poll_entries(const int (&ent)[R], __amdgpu_buffe
   }
 }
 
+// -1: the launch aborts; 1: a member met a quotient dd_check could not prove
+// (exact_div.hpp) — the decode stops like a converged one (the same mailbox
+// flush) and the caller defers the codeword to the barrier-exchange launch on
+// the exact path; 0: done.
 template <int kG, int T, int RV, int RC, int RX, bool SYN>
-__device__ __forceinline__ bool part_iterations_tagged(
+__device__ __forceinline__ int part_iterations_tagged(
     const BpLaunch &a, int M, int cw, GroupSync *gs, unsigned &g, int *sfail, int *sdead, int member,
     unsigned *abort, unsigned char *smem, uint8_t *dec, int NG, __amdgpu_buffer_rsrc_t tb, unsigned tb_c2v,
     const int (&vaddr)[RV][3],
     const bool (&vact)[RV], const double (&pv)[RV], const int (&crow)[RC],
     const int (&cbase)[RC], const int (&crx)[RC], const bool (&cact)[RC], const int (&xr)[RX], const int (&xc)[RX],
-    int odd, int &iter_out, bool &conv_out, int &pcnt_out, int &decbuf_out) {
+    int odd, int &iter_out, bool &conv_out, int &pcnt_out, int &decbuf_out, bool sus0 = false) {
   constexpr int DV = 3, DC = 6, H = 3, NW = T / 64;
   const int tid = threadIdx.x;
   __shared__ int sarrive;  // waves done with the CN phase of this iteration
-  __shared__ int sany;     // some member had failing rows after the previous CN phase
+  __shared__ int sany;     // bit 0: some member had failing rows after the previous CN phase; bit 1: an unproven quotient
   if (tid == 0) sarrive = 0;
   int iter = 0, pcnt_prev = 0;
+  bool sus = sus0;
   double syn_prev[RC];
 #pragma unroll
   for (int r = 0; r < RC; ++r) syn_prev[r] = 0.0;
@@ -992,9 +1032,9 @@ __device__ __forceinline__ bool part_iterations_tagged(
           const double n0 = a0[r] * c0;
           const double n1 = a1[r] * (1.0 - c0);
           if (k + 1 < DV) {
-            div2<true>(n0, n1, n0 + n1, a0[r], a1[r]);
+            div2<true>(n0, n1, n0 + n1, a0[r], a1[r], sus);
           } else {
-            const int hd = hard_decision<true>(n0, n1);
+            const int hd = hard_decision<true>(n0, n1, sus);
             hdb[r] = hd ? kHdHi : 0u;
             if (vact[r]) decb[r * T + tid] = (unsigned char)hd;
           }
@@ -1018,9 +1058,9 @@ __device__ __forceinline__ bool part_iterations_tagged(
           const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
           double q0, q1;
           if (unit)
-            div2<true, true>(t0, t1, t0 + t1, q0, q1);
+            div2<true, true>(t0, t1, t0 + t1, q0, q1, sus);
           else
-            div2<true>(t0, t1, t0 + t1, q0, q1);
+            div2<true>(t0, t1, t0 + t1, q0, q1, sus);
           if (vact[r]) {
             const int x1 = vaddr[r][k] >> 16;  // mailbox index + 1 of a cut edge, 0 for a row slot
             if (x1) {
@@ -1036,7 +1076,7 @@ __device__ __forceinline__ bool part_iterations_tagged(
               b0[r] = c0;
               b1[r] = 1.0 - c0;
             } else {
-              div2<true>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r]);
+              div2<true>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r], sus);
             }
           }
         }
@@ -1048,11 +1088,11 @@ __device__ __forceinline__ bool part_iterations_tagged(
       if (!poll_entries<RX, 2>(xr, tb, 0u, smem, tag, abort)) *sdead = 1;
     KML_STAMP(4);
     if (iter > 0 && tid < 64) {  // wave 0: lane m polls member m's flag of iteration g - 1
-      unsigned long long v = (unsigned long long)g << 1;
+      unsigned long long v = (unsigned long long)g << 2;
       if (tid < kG) {
         for (long long spin = 0;; ++spin) {
           v = spin == 0 ? vflag : ld_rlx64(&gs->mflag[(g - 1) & 1][tid]);  // first: the load issued before VN
-          if ((v >> 1) == (unsigned long long)g) break;
+          if ((v >> 2) == (unsigned long long)g) break;
           if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
             __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             *sdead = 1;
@@ -1061,14 +1101,18 @@ __device__ __forceinline__ bool part_iterations_tagged(
           __builtin_amdgcn_s_sleep(1);
         }
       }
-      const bool any = __ballot((v & 1) != 0) != 0;
-      if (tid == 0) sany = any ? 1 : 0;
+      const int any = (__ballot((v & 1) != 0) != 0 ? 1 : 0) | (__ballot((v & 2) != 0) != 0 ? 2 : 0);
+      if (tid == 0) sany = any;
     }
     __syncthreads();
     KML_STAMP(5);
-    if (*sdead) return false;
-    if (iter > 0 && !sany) {  // every row satisfied after iteration iter - 1: stop before its CN phase
-      conv = true;
+    if (*sdead) return -1;
+    // stop before the CN phase of iteration iter - 1's successor when every row
+    // was satisfied after it, or when a member met an unproven quotient in VN
+    // iter - 1 (then the codeword is redone exactly; the same mailbox flush)
+    const bool suspect = iter > 0 && (sany & 2);
+    if (iter > 0 && (!(sany & 1) || suspect)) {
+      conv = !suspect;
       --iter;
       if (iter + 1 < a.iter_count) {  // VN iter + 1 ran: flush the c2v entries (see above)
         const double dummy = or_hi(0.5, tag ? kTagHi : 0u);
@@ -1085,6 +1129,7 @@ __device__ __forceinline__ bool part_iterations_tagged(
           }
         ++g;
       }
+      if (suspect) return 1;
       break;
     }
     if constexpr (SYN) {  // the previous CN phase counted: its syndromes stand (alpha past the last edge, :274)
@@ -1174,7 +1219,7 @@ __device__ __forceinline__ bool part_iterations_tagged(
             const bool unit = st == 0;
             const double n0 = unit ? m0[r] : s0[r] * m0[r] + s1[r] * m1[r];
             const double n1 = unit ? m1[r] : s0[r] * m1[r] + s1[r] * m0[r];
-            div2<true, true>(n0, n1, n0 + n1, s0[r], s1[r]);
+            div2<true, true>(n0, n1, n0 + n1, s0[r], s1[r], sus);
           }
         }
       }
@@ -1190,14 +1235,14 @@ __device__ __forceinline__ bool part_iterations_tagged(
       nfail += (cact[r] && !odd) ? full : 0;
     }
     pcnt_prev = nfail;  // unsatisfied checks of this iteration's hard decisions (final if the loop ends after it)
-    const bool wfail = __ballot(fail) != 0;
+    const int wbits = (__ballot(fail) != 0 ? 1 : 0) | (__ballot(sus) != 0 ? 2 : 0);
     KML_STAMP(6);
     if ((tid & 63) == 0) {  // the member's last wave to get here posts its flag
-      if (wfail) atomicOr(sfail, 1);
+      if (wbits) atomicOr(sfail, wbits);
       if (atomicAdd(&sarrive, 1) == NW - 1) {
         const int f = atomicExch(sfail, 0);
         sarrive = 0;
-        __hip_atomic_store(&gs->mflag[g & 1][member], ((unsigned long long)(g + 1) << 1) | (unsigned long long)(f != 0),
+        __hip_atomic_store(&gs->mflag[g & 1][member], ((unsigned long long)(g + 1) << 2) | (unsigned long long)(f & 3),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -1207,17 +1252,22 @@ __device__ __forceinline__ bool part_iterations_tagged(
       if (!poll_entries<RX, 1>(xc, tb, tb_c2v, smem, tag, abort)) *sdead = 1;
     __syncthreads();
     KML_STAMP(8);
-    if (*sdead) return false;
+    if (*sdead) return -1;
   }
   iter_out = iter;
   conv_out = conv;
   pcnt_out = conv ? 0 : pcnt_prev;
   decbuf_out = iter & 1;  // the decisions of the last counted VN phase (iteration iter, or iter - 1 at max)
   if (!conv) decbuf_out = (iter - 1) & 1;
-  return true;
+  return 0;
 }
 
-template <int kG, int T, int RV, int RC, int RX, bool SYN, bool TAGGED>
+// Three launches (launch_bp_coop): TAGGED (FAST codewords of same-XCD groups;
+// defers the rest, marking the ones that need the exact path with bit 31),
+// then the barrier-exchange FAST kernel over those (TAGGED = EXACT = false;
+// defers non-FAST and suspect codewords), then the barrier-exchange EXACT
+// kernel over what remains.  Each follow-up launch is usually empty.
+template <int kG, int T, int RV, int RC, int RX, bool SYN, bool TAGGED, bool EXACT>
 __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, GroupSync *gsync, uint8_t *gcch,
                                                     unsigned *abort, unsigned int *queue, int fast_allowed) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1307,12 +1357,15 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;
     const int entry = (int)ld_rlx(&gs->cw);
     if (entry >= B) break;
-    const int cw = a.cw_idx ? a.cw_idx[entry] : entry;
+    // a deferred entry with bit 31 set: a codeword the tagged launch stopped on
+    // an unproven quotient, decoded here on the exact path
+    const int raw = a.cw_idx ? a.cw_idx[entry] : entry;
+    const int cw = raw & 0x7FFFFFFF;
     const double *p0 = a.p0 + (long long)cw * a.p0_stride;
     if (a.p0_sel) p0 += (long long)a.p0_sel[cw] * a.p0_sel_stride;
 
     double pv[RV];
-    bool ok = true;
+    bool ok = raw >= 0;
 #pragma unroll
     for (int r = 0; r < RV; ++r) {
       const int col = c.pt_vn[vpos[r]];
@@ -1324,30 +1377,48 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     if (__ballot(!ok) != 0 && (tid & 63) == 0)
       __hip_atomic_fetch_or(&gs->nofast, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;
-    const bool fast = (fast_allowed & 1) && !ld_rlx(&gs->nofast);
+    const bool fast = !EXACT && (fast_allowed & 1) && !ld_rlx(&gs->nofast);
     constexpr bool tagged = TAGGED;
 
     int iter = 0, pcnt = 0, decbuf = 0;
     bool conv = false;
-    bool alive;
     if constexpr (TAGGED) {
-      if (!fast || !same_xcd) {  // to the barrier-exchange launch
-        if (member == 0 && tid == 0) a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = cw;
+      if (!fast || !same_xcd) {  // to the barrier-exchange launches (bit 31: the exact one)
+        if (member == 0 && tid == 0) a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = fast ? cw : (int)((unsigned)cw | 0x80000000u);
         continue;
       }
-      alive = part_iterations_tagged<kG, T, RV, RC, RX, SYN>(a, c.M, cw, gs, g, &sfail, &sdead, member, abort, smem, dec,
-                                                          NG, tb, tb_c2v, vaddr, vact, pv, crow, cbase, crx, cact,
-                                                          xr, xc, odd, iter, conv, pcnt, decbuf);
-    } else if (fast) {
-      alive = part_iterations<kG, RV, RC, RX, SYN, true>(a, c.M, c.N, NG, cw, gs, bst, nb, &sfail, same_xcd, abort, smem, dec,
-                                                         mb_v2c, mb_c2v, gc, c, vaddr, vpos, vact, pv, crow, cbase,
-                                                         cact, xr, xc, odd, member, iter, conv);
+      const int st = part_iterations_tagged<kG, T, RV, RC, RX, SYN>(a, c.M, cw, gs, g, &sfail, &sdead, member, abort,
+                                                                   smem, dec, NG, tb, tb_c2v, vaddr, vact, pv, crow,
+                                                                   cbase, crx, cact, xr, xc, odd, iter, conv, pcnt,
+                                                                   decbuf, (fast_allowed & 2) != 0);
+      if (st < 0) return;
+      if (st == 1) {  // an unproven quotient: redone by the exact launch (every member took this branch)
+        if (member == 0 && tid == 0) {
+          a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = (int)((unsigned)cw | 0x80000000u);
+          if (a.counters) atomicAdd(&a.counters[CNT_REDONE], 1ull);
+        }
+        continue;
+      }
+    } else if constexpr (!EXACT) {
+      int st = 1;  // 1: to the exact launch
+      if (fast)
+        st = part_iterations<kG, RV, RC, RX, SYN, true>(a, c.M, c.N, NG, cw, gs, bst, nb, &sfail, same_xcd, abort, smem,
+                                                        dec, mb_v2c, mb_c2v, gc, c, vaddr, vpos, vact, pv, crow, cbase,
+                                                        cact, xr, xc, odd, member, iter, conv, (fast_allowed & 2) != 0);
+      if (st < 0) return;
+      if (st == 1) {  // group-wide: nofast, or the suspect count every member read at the same barrier
+        if (member == 0 && tid == 0) {
+          a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = cw;
+          if (fast && a.counters) atomicAdd(&a.counters[CNT_REDONE], 1ull);
+        }
+        continue;
+      }
     } else {
-      alive = part_iterations<kG, RV, RC, RX, SYN, false>(a, c.M, c.N, NG, cw, gs, bst, nb, &sfail, same_xcd, abort, smem, dec,
-                                                          mb_v2c, mb_c2v, gc, c, vaddr, vpos, vact, pv, crow, cbase,
-                                                          cact, xr, xc, odd, member, iter, conv);
+      if (part_iterations<kG, RV, RC, RX, SYN, false>(a, c.M, c.N, NG, cw, gs, bst, nb, &sfail, same_xcd, abort, smem,
+                                                      dec, mb_v2c, mb_c2v, gc, c, vaddr, vpos, vact, pv, crow, cbase,
+                                                      cact, xr, xc, odd, member, iter, conv) < 0)
+        return;
     }
-    if (!alive) return;
 
     // ---- outputs
     if (a.iter_count > 0) {
@@ -1458,9 +1529,9 @@ hipError_t launch_resident(const void *kern, unsigned grid, unsigned block, void
   return hipLaunchCooperativeKernel(kern, dim3(grid), dim3(block), args, lds, s);
 }
 
-template <int kG, int T, int RV, int RC, int RX, bool SYN, bool TAGGED>
+template <int kG, int T, int RV, int RC, int RX, bool SYN, bool TAGGED, bool EXACT>
 hipError_t launch_part_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast, int groups, bool reset_abort) {
-  auto kern = bp_part_kernel<kG, T, RV, RC, RX, SYN, TAGGED>;
+  auto kern = bp_part_kernel<kG, T, RV, RC, RX, SYN, TAGGED, EXACT>;
   const size_t lds = part_lds_bytes(c);
   hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -1479,14 +1550,14 @@ hipError_t launch_part_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int
   uint8_t *gcch = a.gcch;
   unsigned *abort = reinterpret_cast<unsigned *>(gs + groups);
   unsigned int *q = a.queue;
-  int f = fast ? 1 : 0;
+  int f = fast;
   void *args[] = {&cc, &aa, &gs, &gcch, &abort, &q, &f};
   return launch_resident((const void *)kern, (unsigned)(groups * kG), (unsigned)T, args, (unsigned)lds, s);
 }
 
-template <int kG, int T, int RV, int RC, bool SYN>
-hipError_t launch_coop_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast, int groups) {
-  auto kern = bp_coop_kernel<kG, T, RV, RC, SYN>;
+template <int kG, int T, int RV, int RC, bool SYN, bool EXACT>
+hipError_t launch_coop_one(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast, int groups) {
+  auto kern = bp_coop_kernel<kG, T, RV, RC, SYN, EXACT>;
   hipError_t e = hipMemsetAsync(a.queue, 0, sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
   // group blocks, and the abort word unless an unchecked earlier launch may have set it
@@ -1501,6 +1572,49 @@ hipError_t launch_coop_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int
   int f = fast;
   void *args[] = {&cc, &aa, &gs, &gcch, &abort, &q, &f};
   return launch_resident((const void *)kern, (unsigned)(groups * kG), (unsigned)T, args, 0u, s);
+}
+
+// FAST kernel, then the exact kernel over its defer list (bp_regular.hip launch_reg_t)
+template <int kG, int T, int RV, int RC, bool SYN>
+hipError_t launch_coop_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast, int groups) {
+  if (!(fast & 1)) return launch_coop_one<kG, T, RV, RC, SYN, true>(c, a, s, 0, groups);
+  if (!a.defer_idx || !a.defer_cnt) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(a.defer_cnt, 0, sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
+  e = launch_coop_one<kG, T, RV, RC, SYN, false>(c, a, s, fast, groups);
+  if (e != hipSuccess) return e;
+  BpLaunch b = a;
+  b.cw_idx = a.defer_idx;
+  b.B_dev = a.defer_cnt;
+  b.reset_abort = false;  // an abort of the FAST launch stays visible
+  return launch_coop_one<kG, T, RV, RC, SYN, true>(c, b, s, 0, groups);
+}
+
+// The partitioned kernel's launches for one batch.  a.defer_* (the caller's
+// list) receives the codewords for the exact launch; d.defer_* (scratch past
+// the groups' mailboxes) the tagged launch's deferrals.
+template <int T_, int R_, int X_, bool SYN>
+hipError_t launch_part_chain(const DevCode &c, const BpLaunch &a, const BpLaunch &d, hipStream_t s, int fast, int groups,
+                             bool tagged) {
+  if (!(fast & 1)) return launch_part_t<kPartG, T_, R_, R_, X_, SYN, false, true>(c, a, s, 0, groups, a.reset_abort);
+  if (!a.defer_idx || !a.defer_cnt) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(a.defer_cnt, 0, sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
+  BpLaunch bf = a;  // barrier-exchange FAST launch: the whole batch, or the tagged launch's deferrals
+  bool reset = a.reset_abort;
+  if (tagged) {
+    e = launch_part_t<kPartG, T_, R_, R_, X_, SYN, true, false>(c, d, s, fast, groups, reset);
+    if (e != hipSuccess) return e;
+    bf.cw_idx = d.defer_idx;
+    bf.B_dev = d.defer_cnt;
+    reset = false;  // an abort of an earlier launch stays visible
+  }
+  e = launch_part_t<kPartG, T_, R_, R_, X_, SYN, false, false>(c, bf, s, fast, groups, reset);
+  if (e != hipSuccess) return e;
+  BpLaunch be = a;  // exact launch over what the FAST launches deferred
+  be.cw_idx = a.defer_idx;
+  be.B_dev = a.defer_cnt;
+  return launch_part_t<kPartG, T_, R_, R_, X_, SYN, false, true>(c, be, s, 0, groups, false);
 }
 
 // Kernel choice and tiling.  Default: the partitioned kernel (groups of 4,
@@ -1578,7 +1692,7 @@ hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s) {
   if (groups <= 0 || !a.gsync || !a.gcch || (long long)groups * c.E > a.gslots_cap) return hipErrorNotSupported;
   if (const char *k = getenv("KML_BP_KERNEL"))
     if (k[0] == 'g') return hipErrorNotSupported;
-  const int fast = c.dv_max <= kFastMaxColumnDegree ? 1 : 0;
+  const int fast = bp_fast_mode(c);
   const CoopCfg k = coop_cfg(c);
   if (k.part) {
     // exchange entries per thread: every member's lists must fit RX * T
@@ -1598,21 +1712,10 @@ hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s) {
       hipError_t e = hipMemsetAsync(d.defer_cnt, 0, sizeof(unsigned), s);
       if (e != hipSuccess) return e;
     }
-#define KML_PART_CASE(T_, R_, X_)                                                                   \
-  if (k.T == T_ && xmax <= X_ * T_) {                                                              \
-    if (tagged) {                                                                                  \
-      hipError_t e = a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true, true>(c, d, s, fast, groups, a.reset_abort)   \
-                           : launch_part_t<kPartG, T_, R_, R_, X_, false, true>(c, d, s, fast, groups, a.reset_abort); \
-      if (e != hipSuccess) return e;                                                               \
-      BpLaunch b = a;                                                                              \
-      b.cw_idx = d.defer_idx;                                                                      \
-      b.B_dev = d.defer_cnt;                                                                       \
-      return a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true, false>(c, b, s, fast, groups, false)          \
-                   : launch_part_t<kPartG, T_, R_, R_, X_, false, false>(c, b, s, fast, groups, false);        \
-    }                                                                                              \
-    return a.syn ? launch_part_t<kPartG, T_, R_, R_, X_, true, false>(c, a, s, fast, groups, a.reset_abort)    \
-                 : launch_part_t<kPartG, T_, R_, R_, X_, false, false>(c, a, s, fast, groups, a.reset_abort);  \
-  }
+#define KML_PART_CASE(T_, R_, X_) \
+  if (k.T == T_ && xmax <= X_ * T_)   \
+    return a.syn ? launch_part_chain<T_, R_, X_, true>(c, a, d, s, fast, groups, tagged) \
+                 : launch_part_chain<T_, R_, X_, false>(c, a, d, s, fast, groups, tagged);
     KML_PART_CASE(512, 4, 4)
     KML_PART_CASE(768, 3, 3)
     KML_PART_CASE(1024, 2, 2)

@@ -58,7 +58,7 @@ __device__ __forceinline__ int swap_pair_i(int x) { return __builtin_amdgcn_mov_
 // interleaved step by step so the dependent fma / rcp sequences overlap.
 template <int D, int R, bool FAST>
 __device__ __forceinline__ void vn_cols(double2 *slots, const unsigned short *const (&cs)[R], const double (&p)[R],
-                                        unsigned char *const (&hard)[R]) {
+                                        unsigned char *const (&hard)[R], bool &sus) {
   double c0s[R][D];
 #pragma unroll
   for (int r = 0; r < R; ++r)
@@ -80,9 +80,9 @@ __device__ __forceinline__ void vn_cols(double2 *slots, const unsigned short *co
       const double n0 = a0[r] * c0s[r][k];
       const double n1 = a1[r] * (1.0 - c0s[r][k]);
       if (k + 1 < D)
-        div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r]);
+        div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r], sus);
       else
-        *hard[r] = (unsigned char)(hb[r] = hard_decision<FAST>(n0, n1));
+        *hard[r] = (unsigned char)(hb[r] = hard_decision<FAST>(n0, n1, sus));
     }
   double b0[R], b1[R];
 #pragma unroll
@@ -96,9 +96,9 @@ __device__ __forceinline__ void vn_cols(double2 *slots, const unsigned short *co
       const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
       double q0, q1;
       if (unit)  // beta = (1, 1): t is the normalised alpha, its sum within ulps of 1 (bp_common.hpp rcp_near1)
-        div2<FAST, true>(t0, t1, t0 + t1, q0, q1);
+        div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
       else
-        div2<FAST>(t0, t1, t0 + t1, q0, q1);
+        div2<FAST>(t0, t1, t0 + t1, q0, q1, sus);
       // the column's decision rides in the sign bit of the v2c q1 (a probability,
       // so the bit is otherwise clear): the parity check reads it in row order
       slots[cs[r][k]] = make_double2(q0, with_sign(q1, hb[r]));
@@ -108,7 +108,7 @@ __device__ __forceinline__ void vn_cols(double2 *slots, const unsigned short *co
           b0[r] = c0;
           b1[r] = 1.0 - c0;
         } else {
-          div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r]);
+          div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r], sus);
         }
       }
     }
@@ -213,22 +213,22 @@ __device__ __forceinline__ void set_prio(int p) {
 // per SIMD holds two interleaved chains only up to those degrees.
 template <int D, int R, bool FAST>
 __device__ __forceinline__ void vn_cols_if(double2 *slots, const unsigned short *const (&cs)[R], const double (&p)[R],
-                                           unsigned char *const (&h)[R]) {
-  if constexpr (R == 1 || D <= kIrrVnPairMax) vn_cols<D, R, FAST>(slots, cs, p, h);
+                                           unsigned char *const (&h)[R], bool &sus) {
+  if constexpr (R == 1 || D <= kIrrVnPairMax) vn_cols<D, R, FAST>(slots, cs, p, h, sus);
 }
 template <int R, bool FAST>
 __device__ __forceinline__ void vn_any(int d, double2 *slots, const unsigned short *const (&cs)[R], const double (&p)[R],
-                                       unsigned char *const (&h)[R]) {
+                                       unsigned char *const (&h)[R], bool &sus) {
   switch (d) {
-    case 1: vn_cols_if<1, R, FAST>(slots, cs, p, h); break;
-    case 2: vn_cols_if<2, R, FAST>(slots, cs, p, h); break;
-    case 3: vn_cols_if<3, R, FAST>(slots, cs, p, h); break;
-    case 4: vn_cols_if<4, R, FAST>(slots, cs, p, h); break;
-    case 5: vn_cols_if<5, R, FAST>(slots, cs, p, h); break;
-    case 6: vn_cols_if<6, R, FAST>(slots, cs, p, h); break;
-    case 7: vn_cols_if<7, R, FAST>(slots, cs, p, h); break;
-    case 8: vn_cols_if<8, R, FAST>(slots, cs, p, h); break;
-    default: vn_cols_if<9, R, FAST>(slots, cs, p, h); break;
+    case 1: vn_cols_if<1, R, FAST>(slots, cs, p, h, sus); break;
+    case 2: vn_cols_if<2, R, FAST>(slots, cs, p, h, sus); break;
+    case 3: vn_cols_if<3, R, FAST>(slots, cs, p, h, sus); break;
+    case 4: vn_cols_if<4, R, FAST>(slots, cs, p, h, sus); break;
+    case 5: vn_cols_if<5, R, FAST>(slots, cs, p, h, sus); break;
+    case 6: vn_cols_if<6, R, FAST>(slots, cs, p, h, sus); break;
+    case 7: vn_cols_if<7, R, FAST>(slots, cs, p, h, sus); break;
+    case 8: vn_cols_if<8, R, FAST>(slots, cs, p, h, sus); break;
+    default: vn_cols_if<9, R, FAST>(slots, cs, p, h, sus); break;
   }
 }
 
@@ -279,10 +279,15 @@ __device__ unsigned long long kml_irr_stamps[kIrrThreads / 64][8];
 
 // Column / row of the lane in round r of the plan (layout.hpp IrregularPlan):
 // rounds 0 and 1 pair two items of one degree, round 2 holds single items.
+// Returns true when a FAST decode met an unproven quotient (exact_div.hpp):
+// the caller re-initialises the slots and redoes the codeword with FAST =
+// false (decided at the CN closing barrier, before that iteration's
+// syndromes are written; see bp_regular.hip decode_reg).
 template <int T, bool SYN, bool FAST>
-__device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, int cw, double2 *slots,
+__device__ __forceinline__ bool decode_irr(const DevCode &c, const BpLaunch &a, int cw, double2 *slots,
                                            const unsigned short *cslot, const double *p0s, unsigned char *cch, int odd,
-                                           const int (&vcol)[3], const int (&crow)[3], int &iter_out, bool &conv_out) {
+                                           const int (&vcol)[3], const int (&crow)[3], int &iter_out, bool &conv_out,
+                                           bool sus0 = false) {
   // Each lane's plan packed into one word per round (slot base | degree << 14
   // | column or row << 18; ~0 = no item), built once per codeword: the
   // iteration loop makes no global loads.  The words are laundered at the top
@@ -308,7 +313,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
   auto pitem = [](unsigned w) { return (int)(w >> 18); };
   __shared__ __attribute__((aligned(16))) int wflags[16];  // wg_any (bp_common.hpp)
   int iter = 0;
-  bool conv = false;
+  bool conv = false, sus = sus0;
   auto prior = [&](int v) { return v >= c.punct ? p0s[v - c.punct] : 0.5; };  // :126-134
 #if KML_STAMPS
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
@@ -330,7 +335,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
       const unsigned short *const cs[2] = {cslot + pbase(vp[0]), cslot + pbase(vp[1])};
       const double p[2] = {prior(v0), prior(v1)};
       unsigned char *const h[2] = {&cch[v0], &cch[v1]};
-      vn_any<2, FAST>(pdeg(vp[0]), slots, cs, p, h);
+      vn_any<2, FAST>(pdeg(vp[0]), slots, cs, p, h, sus);
     }
     IRR_STAMP(0);
     set_prio(KML_IRR_PRIO_VN_SINGLE);
@@ -339,7 +344,7 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
       const unsigned short *const cs[1] = {cslot + pbase(vp[2])};
       const double p[1] = {prior(v)};
       unsigned char *const h[1] = {&cch[v]};
-      vn_any<1, FAST>(pdeg(vp[2]), slots, cs, p, h);
+      vn_any<1, FAST>(pdeg(vp[2]), slots, cs, p, h, sus);
     }
     IRR_STAMP(1);
     __syncthreads();
@@ -386,7 +391,13 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
       if (cp[r] != ~0u) fail |= full;
     }
     IRR_STAMP(5);
-    if (!wg_any<T / 64>(fail, wflags)) {
+    const int wg = FAST ? wg_any2<T / 64>(fail, sus, wflags) : wg_any<T / 64>(fail, wflags);
+    if (FAST && (wg & 2)) {  // an unproven quotient in this VN phase: redo exactly
+      iter_out = iter;
+      conv_out = false;
+      return true;
+    }
+    if (!(wg & 1)) {
       conv = true;
       break;
     }
@@ -405,9 +416,12 @@ __device__ __forceinline__ void decode_irr(const DevCode &c, const BpLaunch &a, 
 #endif
   iter_out = iter;
   conv_out = conv;
+  return false;
 }
 
-template <int T, bool SYN>
+// EXACT = false: the FAST kernel (defers non-FAST and suspect codewords);
+// EXACT = true: the exact path over the defer list (see bp_regular.hip).
+template <int T, bool SYN, bool EXACT>
 __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, unsigned int *queue, int fast_allowed) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) int pflags[16];  // wg_all of the FAST prior check (bp_common.hpp)
@@ -428,6 +442,7 @@ __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, 
     crow[r] = c.irr_cn[r * (T / 2) + (tid >> 1)];
   }
 
+  const int B = a.B_dev ? (int)*a.B_dev : a.B;  // the exact kernel: the FAST kernel's defer count
   for (;;) {
     __syncthreads();
     if (tid == 0) {
@@ -437,7 +452,7 @@ __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, 
     }
     __syncthreads();
     const int entry = red[3];
-    if (entry >= a.B) break;
+    if (entry >= B) break;
     const int cw = a.cw_idx ? a.cw_idx[entry] : entry;
     const double *p0 = a.p0 + (long long)cw * a.p0_stride;
     if (a.p0_sel) p0 += (long long)a.p0_sel[cw] * a.p0_sel_stride;
@@ -449,14 +464,24 @@ __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, 
       ok = ok && fast_prior_ok(q);
     }
     for (int e = tid; e < c.irr_slots; e += T) slots[e].x = 0.5;  // InitMsg
-    const bool fast = wg_all<T / 64>(ok ? 1 : 0, pflags) && fast_allowed;
+    const bool fast = wg_all<T / 64>(ok ? 1 : 0, pflags) && (fast_allowed & 1);
 
     int iter = 0;
     bool conv = false;
-    if (fast)
-      decode_irr<T, SYN, true>(c, a, cw, slots, cslot, p0s, cch, odd, vcol, crow, iter, conv);
-    else
+    if constexpr (!EXACT) {
+      bool defer = !fast;
+      if (fast && decode_irr<T, SYN, true>(c, a, cw, slots, cslot, p0s, cch, odd, vcol, crow, iter, conv,
+                                           (fast_allowed & 2) != 0)) {
+        defer = true;  // an unproven quotient: the exact kernel redoes the codeword
+        if (tid == 0 && a.counters) atomicAdd(&a.counters[CNT_REDONE], 1ull);
+      }
+      if (defer) {
+        if (tid == 0) a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = cw;
+        continue;
+      }
+    } else {
       decode_irr<T, SYN, false>(c, a, cw, slots, cslot, p0s, cch, odd, vcol, crow, iter, conv);
+    }
 
     if (a.iter_count > 0) {
       if (a.uu_hat) {
@@ -509,9 +534,9 @@ size_t irr_lds_bytes(const DevCode &c) {
   return (size_t)c.irr_slots * 16 + (size_t)c.E * 2 + (size_t)c.cc_len * 8 + kRedBytes + (size_t)c.N;
 }
 
-template <int T, bool SYN>
-hipError_t launch_irr_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
-  auto kern = bp_irregular_kernel<T, SYN>;
+template <int T, bool SYN, bool EXACT>
+hipError_t launch_irr_one(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
+  auto kern = bp_irregular_kernel<T, SYN, EXACT>;
   const size_t lds = irr_lds_bytes(c);
   hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -526,13 +551,28 @@ hipError_t launch_irr_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int 
   return hipGetLastError();
 }
 
+// FAST kernel, then the exact kernel over its defer list (bp_regular.hip launch_reg_t)
+template <int T, bool SYN>
+hipError_t launch_irr_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
+  if (!(fast_allowed & 1)) return launch_irr_one<T, SYN, true>(c, a, s, 0);
+  if (!a.defer_idx || !a.defer_cnt) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(a.defer_cnt, 0, sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
+  e = launch_irr_one<T, SYN, false>(c, a, s, fast_allowed);
+  if (e != hipSuccess) return e;
+  BpLaunch b = a;
+  b.cw_idx = a.defer_idx;
+  b.B_dev = a.defer_cnt;
+  return launch_irr_one<T, SYN, true>(c, b, s, 0);
+}
+
 }  // namespace
 
 hipError_t launch_bp_irregular(const DevCode &c, const BpLaunch &a, hipStream_t s) {
   constexpr int T = kIrrThreads;
   if (irr_lds_bytes(c) > 160 * 1024 || c.irr_slots > 16383) return hipErrorNotSupported;
   if (!c.irr_ok || !c.irr_vn) return hipErrorNotSupported;
-  const int fast = c.dv_max <= kFastMaxColumnDegree ? 1 : 0;
+  const int fast = bp_fast_mode(c);
   return a.syn ? launch_irr_t<T, true>(c, a, s, fast) : launch_irr_t<T, false>(c, a, s, fast);
 }
 

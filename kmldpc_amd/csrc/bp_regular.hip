@@ -108,16 +108,23 @@ __device__ __forceinline__ double with_sign(double x, int bit) {
   return __hiloint2double((__double2hiint(x) & 0x7FFFFFFF) | (bit << 31), __double2loint(x));
 }
 
+// Returns true when a FAST decode met a quotient dd_check could not prove
+// correctly rounded (exact_div.hpp): the caller redoes the codeword with
+// FAST = false.  The decision is taken at the CN phase's closing barrier,
+// before that iteration's syndromes are written, so everything a suspect
+// decode wrote (slots, decisions, syndromes of earlier iterations) is what the
+// exact decode rewrites identically or overwrites.
 template <int T, int RV, int RC, int DV, int DC, bool SYN, bool FAST>
-__device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, int cw, unsigned char *smem,
+__device__ __forceinline__ bool decode_reg(const DevCode &c, const BpLaunch &a, int cw, unsigned char *smem,
                                            unsigned hd, const unsigned (&vaddr)[RV][DV], const double (&pv)[RV],
                                            const int (&crow)[RC], const unsigned (&rb)[RC], const unsigned (&rb2)[RC],
-                                           const unsigned (&wb)[RC], int odd, int &iter_out, bool &conv_out) {
+                                           const unsigned (&wb)[RC], int odd, int &iter_out, bool &conv_out,
+                                           bool sus0 = false) {
   static_assert(DC % 2 == 0, "the lane-pair split assumes an even row degree");
   constexpr int H = DC / 2;
   __shared__ __attribute__((aligned(16))) int wflags[16];  // wg_any (bp_common.hpp)
   int iter = 0;
-  bool conv = false;
+  bool conv = false, sus = sus0;
 #if KML_STAMPS
   unsigned long long ws_acc[4] = {0, 0, 0, 0}, ws_prev = __builtin_amdgcn_s_memtime();
 #endif
@@ -166,9 +173,9 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
           const double n0 = a0[r] * c0;
           const double n1 = a1[r] * (1.0 - c0);
           if (k + 1 < DV)
-            div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r]);
+            div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r], sus);
           else {  // the posterior only feeds the hard decision
-            hb[r] = hard_decision<FAST>(n0, n1);
+            hb[r] = hard_decision<FAST>(n0, n1, sus);
             lds_st<unsigned char>(hd + r * T, (unsigned char)hb[r]);
           }
         }
@@ -191,9 +198,9 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
           const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
           double q0, q1;
           if (unit)  // beta = (1, 1): t is the normalised alpha, its sum within ulps of 1 (bp_common.hpp rcp_near1)
-            div2<FAST, true>(t0, t1, t0 + t1, q0, q1);
+            div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
           else
-            div2<FAST>(t0, t1, t0 + t1, q0, q1);
+            div2<FAST>(t0, t1, t0 + t1, q0, q1, sus);
           // the column's decision rides in the sign bit of q1 (a probability,
           // >= +0): the CN chains that load the message collect the parity
           lds_st<dbl2>(vaddr[r][k] & ~15u, dbl2{q0, with_sign(q1, hb[r])});
@@ -203,7 +210,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
               b0[r] = c0;
               b1[r] = 1.0 - c0;
             } else {
-              div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r]);
+              div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r], sus);
             }
           }
         }
@@ -313,9 +320,14 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
       fail |= p ^ swap_pair_i(p);
     }
     REG_WSTAMP(2);
-    const int any_fail = wg_any<T / 64>(fail, wflags);
+    const int wg = FAST ? wg_any2<T / 64>(fail, sus, wflags) : wg_any<T / 64>(fail, wflags);
     REG_WSTAMP(3);
-    if (!any_fail) {  // every row satisfied before this CN phase
+    if (FAST && (wg & 2)) {  // an unproven quotient in this VN phase: redo exactly
+      iter_out = iter;
+      conv_out = false;
+      return true;
+    }
+    if (!(wg & 1)) {  // every row satisfied before this CN phase
       conv = true;
       break;
     }
@@ -331,6 +343,7 @@ __device__ __forceinline__ void decode_reg(const DevCode &c, const BpLaunch &a, 
 #endif
   iter_out = iter;
   conv_out = conv;
+  return false;
 }
 
 // Dynamic LDS: E slots of 16 B, the reduction words, N hard-decision bytes,
@@ -343,7 +356,14 @@ constexpr size_t ipos_offset(int E, int N, int DMB) {
 }
 constexpr size_t reg_lds_bytes(int E, int N, int K, int DMB) { return ipos_offset(E, N, DMB) + (size_t)K * 2; }
 
-template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB>
+// EXACT = false: the FAST kernel.  It decodes every codeword whose priors
+// qualify (bp_common.hpp fast_prior_ok) on the FAST path and appends the rest,
+// and every codeword whose FAST decode met an unproven quotient, to the defer
+// list (a.defer_idx / a.defer_cnt; no outputs, no counters for those).
+// EXACT = true: decodes its entries (the defer list) on the exact path (div_rn).
+// Two kernels rather than one with both paths: the exact path's registers
+// would otherwise be allocated (and spilled) in the FAST kernel too.
+template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB, bool EXACT>
 __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, unsigned int *queue, int fast_allowed) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) int pflags[16];  // wg_all of the FAST prior check (bp_common.hpp)
@@ -395,6 +415,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
 #if KML_STAMPS
   unsigned long long rs_prev = __builtin_amdgcn_s_memtime(), rs_acc[8] = {};
 #endif
+  const int B = a.B_dev ? (int)*a.B_dev : a.B;  // the exact kernel: the FAST kernel's defer count
   for (;;) {
     __syncthreads();
     if (tid == 0) {
@@ -405,9 +426,10 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
     __syncthreads();
     const int entry = red[3];
     REG_STAMP(0);
-    if (entry >= a.B) break;
+    if (entry >= B) break;
     const int cw = a.cw_idx ? a.cw_idx[entry] : entry;
     const double *p0;
+    bool dok = true;  // FAST kernel: every symbol's FAST demap proven (else the exact kernel demaps the codeword)
     if constexpr (DMB > 0) {  // ModemLinearSystem::DeMapping of this codeword into LDS
       const int S = c.cc_len / DMB;
       const double2 hh = a.sym_h[(long long)cw * a.sym_h_stride + (a.sym_h_sel ? a.sym_h_sel[cw] : 0)];
@@ -415,7 +437,10 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
       for (int j = tid; j < S; j += T) {
         const double2 v = yy[j];
         double out[DMB];
-        demap_symbol<DMB>((lds_cons)dcons, (lds_exptab)detab, v.x, v.y, hh.x, hh.y, a.sym_var, out);
+        if constexpr (EXACT)
+          demap_symbol<DMB>((lds_cons)dcons, (lds_exptab)detab, v.x, v.y, hh.x, hh.y, a.sym_var, out);
+        else  // no exact fallback in the FAST kernel (its registers): a failing symbol defers the codeword
+          dok &= demap_symbol_t<DMB, true>((lds_cons)dcons, (lds_exptab)detab, v.x, v.y, hh.x, hh.y, a.sym_var, out);
 #pragma unroll
         for (int b = 0; b < DMB; ++b) p0s[j * DMB + b] = out[b];
       }
@@ -428,22 +453,32 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
 
     REG_STAMP(1);
     double pv[RV];
-    bool ok = true;
+    bool ok = dok;
 #pragma unroll
     for (int r = 0; r < RV; ++r) {
       pv[r] = (vcol[r] >= c.punct) ? p0[vcol[r] - c.punct] : 0.5;
       ok = ok && fast_prior_ok(pv[r]);
     }
-    const bool fast = wg_all<T / 64>(ok ? 1 : 0, pflags) && fast_allowed;
+    const bool fast = wg_all<T / 64>(ok ? 1 : 0, pflags) && (fast_allowed & 1);
     REG_STAMP(2);
 
     int iter = 0;
     bool conv = false;
-    if (fast)
-      decode_reg<T, RV, RC, DV, DC, SYN, true>(c, a, cw, smem, cch_a + tid, vaddr, pv, crow, rb, rb2, wb, odd, iter, conv);
-    else
+    if constexpr (!EXACT) {
+      bool defer = !fast;
+      if (fast && decode_reg<T, RV, RC, DV, DC, SYN, true>(c, a, cw, smem, cch_a + tid, vaddr, pv, crow, rb, rb2, wb,
+                                                           odd, iter, conv, (fast_allowed & 2) != 0)) {
+        defer = true;  // an unproven quotient: the exact kernel redoes the codeword
+        if (tid == 0 && a.counters) atomicAdd(&a.counters[CNT_REDONE], 1ull);
+      }
+      if (defer) {
+        if (tid == 0) a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = cw;
+        continue;
+      }
+    } else {
       decode_reg<T, RV, RC, DV, DC, SYN, false>(c, a, cw, smem, cch_a + tid, vaddr, pv, crow, rb, rb2, wb, odd, iter,
                                                conv);
+    }
 
     REG_STAMP(3);
 #if KML_STAMPS
@@ -521,11 +556,10 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
 #endif
 }
 
-template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB>
-hipError_t launch_reg_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
-  auto kern = bp_regular_kernel<T, RV, RC, DV, DC, SYN, DMB>;
+template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB, bool EXACT>
+hipError_t launch_reg_one(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
+  auto kern = bp_regular_kernel<T, RV, RC, DV, DC, SYN, DMB, EXACT>;
   const size_t lds = reg_lds_bytes(c.E, c.N, c.K, DMB);
-  if (lds > 160 * 1024 || c.K > 65536 || c.N > 65536) return hipErrorNotSupported;
   hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   int dev = 0, ncu = 0;
@@ -537,6 +571,25 @@ hipError_t launch_reg_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int 
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(T), lds, s, c, a, a.queue, fast_allowed);
   return hipGetLastError();
+}
+
+// The FAST kernel over the batch, then the exact kernel over the codewords it
+// deferred (usually none: its workgroups read a zero count and leave); with
+// FAST division off, the exact kernel over the batch.
+template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB>
+hipError_t launch_reg_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
+  const size_t lds = reg_lds_bytes(c.E, c.N, c.K, DMB);
+  if (lds > 160 * 1024 || c.K > 65536 || c.N > 65536) return hipErrorNotSupported;
+  if (!(fast_allowed & 1)) return launch_reg_one<T, RV, RC, DV, DC, SYN, DMB, true>(c, a, s, 0);
+  if (!a.defer_idx || !a.defer_cnt) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(a.defer_cnt, 0, sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
+  e = launch_reg_one<T, RV, RC, DV, DC, SYN, DMB, false>(c, a, s, fast_allowed);
+  if (e != hipSuccess) return e;
+  BpLaunch b = a;
+  b.cw_idx = a.defer_idx;
+  b.B_dev = a.defer_cnt;
+  return launch_reg_one<T, RV, RC, DV, DC, SYN, DMB, true>(c, b, s, 0);
 }
 
 }  // namespace
@@ -551,7 +604,7 @@ int bp_regular_threads(int N, int M, int E, int dv_max, int dc_max, int regular)
 hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s) {
   if (!c.reg_c2v || bp_regular_threads(c.N, c.M, c.E, c.dv_max, c.dc_max, c.regular) != 768)
     return hipErrorNotSupported;
-  const int fast = c.dv_max <= kFastMaxColumnDegree ? 1 : 0;
+  const int fast = bp_fast_mode(c);
   if (a.sym_y) {
     if (!bp_regular_fuses_demap(c, a.sym_bits) || a.cw_idx || a.p0_sel) return hipErrorNotSupported;
     return a.syn ? launch_reg_t<768, 3, 3, 3, 6, true, 2>(c, a, s, fast)

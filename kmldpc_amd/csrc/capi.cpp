@@ -12,6 +12,7 @@
 
 #include "../../include/kmldpc_amd.h"
 #include "code.hpp"
+#include "comm.hpp"
 #include "config.hpp"
 #include "kernels.hpp"
 #include "layout.hpp"
@@ -86,6 +87,9 @@ struct kml_ctx {
   long long part_cut = 0;   // cut edges of the partition plan (partitioned cooperative kernel)
   bool coop_pending = false;  // a cooperative launch whose abort word is unchecked
   int inject_abort = -1;      // test hook (kml_debug_inject_abort): raise the abort after the n-th coop launch
+  kml::RcclComm *comm = nullptr;  // counter all-reduce over the ranks (kml_comm_init)
+  DBuf w_comm;
+  DBuf w_defer;  // BP launches: codewords the FAST kernel leaves to the exact kernel (+ count)
   // workspaces
   DBuf w_y, w_h, w_h4, w_hhat, w_p0, w_uu, w_uh, w_uh4, w_ret, w_cch, w_syn, w_sel, w_met, w_pc, w_cnt, w_km, w_cwerr;
   // soft syndrome metric: candidate / final syndromes, iteration counts, sums, decode lists
@@ -385,6 +389,9 @@ int run_bp(kml_ctx *c, kml::BpLaunch a, int &slot_out, int reuse = -1) {
   if (reuse < 0)
     HIPCHK(c, hipMemsetAsync(slot_ptr(c, slot), 0, sizeof(unsigned long long) * kml::CNT_N, c->stream), "memset");
   a.counters = slot_ptr(c, slot);
+  HIPCHK(c, c->w_defer.ensure(sizeof(int32_t) * ((size_t)a.B + 16)), "hipMalloc(defer list)");
+  a.defer_idx = c->w_defer.as<int32_t>();
+  a.defer_cnt = reinterpret_cast<unsigned *>(c->w_defer.as<int32_t>() + a.B);
   a.gslots = c->d_gslots.as<double2>();
   a.gslots_cap = c->gslots_cap;
   a.queue = c->d_queue.as<unsigned int>();
@@ -878,6 +885,10 @@ void kml_destroy(kml_ctx *c) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     drain_profile(c);
+    kml::rccl_destroy(c->comm);
+    c->comm = nullptr;
+    c->w_comm.release();
+    c->w_defer.release();
     for (DBuf *b : {&c->d_graph, &c->d_cons, &c->d_arena, &c->d_queue, &c->d_gslots, &c->d_gsync, &c->d_gcch, &c->w_y, &c->w_h, &c->w_h4,
                     &c->w_hhat, &c->w_p0, &c->w_uu, &c->w_uh, &c->w_uh4, &c->w_cwerr, &c->w_ret, &c->w_cch, &c->w_syn, &c->w_sel, &c->w_met,
                     &c->w_pc, &c->w_cnt, &c->w_km, &c->s_synm, &c->s_synf, &c->s_itm, &c->s_itf, &c->s_Lm, &c->s_Lf, &c->s_list, &c->s_sel, &c->s_uu, &c->s_cc, &c->s_y, &c->s_h, &c->w_hc})
@@ -1215,6 +1226,44 @@ int decode_frames_chunked(kml_ctx *c, const double *y, const double *true_h, dou
   return rc;
 }
 }  // namespace
+
+int kml_comm_unique_id(uint8_t *id) {
+  std::string err;
+  if (!id) return KML_E_ARG;
+  return kml::rccl_unique_id(id, err) == 0 ? KML_OK : KML_E_UNSUP;
+}
+
+int kml_comm_init(kml_ctx *c, const uint8_t *id, int world, int rank) {
+  if (!c || !id || world < 1 || rank < 0 || rank >= world) return fail(c, KML_E_ARG, "kml_comm_init: bad argument");
+  TRY(need_gpu(c));
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  if (c->comm) return fail(c, KML_E_ARG, "kml_comm_init: the context already has a communicator");
+  std::string err;
+  c->comm = kml::rccl_init(id, world, rank, err);
+  return c->comm ? KML_OK : fail(c, KML_E_UNSUP, err);
+}
+
+int kml_comm_size(const kml_ctx *c) { return c ? kml::rccl_size(c->comm) : 0; }
+
+namespace {
+int comm_allreduce(kml_ctx *c, void *vals, int n, bool f64) {
+  if (!c || (!vals && n > 0) || n < 0) return fail(c, KML_E_ARG, "kml_comm_allreduce: bad argument");
+  if (!c->comm) return fail(c, KML_E_ARG, "kml_comm_allreduce: no communicator (kml_comm_init)");
+  if (n == 0) return KML_OK;
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const size_t bytes = (size_t)n * 8;
+  HIPCHK(c, c->w_comm.ensure(bytes), "hipMalloc(comm)");
+  HIPCHK(c, hipMemcpyAsync(c->w_comm.p, vals, bytes, hipMemcpyHostToDevice, c->stream), "H2D");
+  std::string err;
+  if (kml::rccl_allreduce(c->comm, c->w_comm.p, (size_t)n, f64, c->stream, err) != 0) return fail(c, KML_E_HIP, err);
+  HIPCHK(c, hipMemcpyAsync(vals, c->w_comm.p, bytes, hipMemcpyDeviceToHost, c->stream), "D2H");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  return KML_OK;
+}
+}  // namespace
+
+int kml_comm_allreduce_u64(kml_ctx *c, uint64_t *vals, int n) { return comm_allreduce(c, vals, n, false); }
+int kml_comm_allreduce_f64(kml_ctx *c, double *vals, int n) { return comm_allreduce(c, vals, n, true); }
 
 int kml_debug_inject_abort(kml_ctx *c, int nth) {
   if (!c) return KML_E_ARG;
@@ -1587,9 +1636,9 @@ int kml_div_probe(kml_ctx *c, const double *in, int n, double *out) {
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
   const double *d_in;
   TRY(stage_in(c, c->w_y, in, (size_t)n * 3, 0, d_in));
-  HIPCHK(c, c->w_p0.ensure(sizeof(double) * 8 * (size_t)n), "hipMalloc");
+  HIPCHK(c, c->w_p0.ensure(sizeof(double) * 11 * (size_t)n), "hipMalloc");
   HIPCHK(c, kml::launch_div_probe(d_in, n, c->w_p0.as<double>(), c->stream), "div probe");
-  TRY(copy_out(c, out, (const double *)c->w_p0.as<double>(), (size_t)n * 8, 0));
+  TRY(copy_out(c, out, (const double *)c->w_p0.as<double>(), (size_t)n * 11, 0));
   return sync(c);
 }
 

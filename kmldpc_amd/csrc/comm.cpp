@@ -1,0 +1,119 @@
+// comm.cpp — the multi-GPU counter all-reduce over RCCL (xGMI), the only
+// collective of the path (the reference's per-thread counters are
+// summed under a mutex, lib/lab/src/threadsafe_sourcesink.cc).
+//
+// The product library talks to RCCL itself, on the context's own HIP stream
+// and through the same HIP runtime as its kernels: the Python drivers use
+// torch.distributed (gloo) only for rendezvous and CPU control (barriers, the
+// unique id's broadcast, the timing gather).  librccl is opened on first use
+// (dlopen), so a host without it, or a single-GPU run, never loads it.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <string>
+
+#include "comm.hpp"
+
+namespace kml {
+
+namespace {
+
+struct RcclApi {
+  bool tried = false, ok = false;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) init_rank = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  std::string why;
+};
+
+RcclApi &api() {
+  static RcclApi a;
+  if (a.tried) return a;
+  a.tried = true;
+  void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    a.why = std::string("cannot load librccl.so.1: ") + dlerror();
+    return a;
+  }
+  a.get_unique_id = reinterpret_cast<decltype(a.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+  a.init_rank = reinterpret_cast<decltype(a.init_rank)>(dlsym(h, "ncclCommInitRank"));
+  a.all_reduce = reinterpret_cast<decltype(a.all_reduce)>(dlsym(h, "ncclAllReduce"));
+  a.destroy = reinterpret_cast<decltype(a.destroy)>(dlsym(h, "ncclCommDestroy"));
+  a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(h, "ncclGetErrorString"));
+  a.ok = a.get_unique_id && a.init_rank && a.all_reduce && a.destroy && a.error_string;
+  if (!a.ok) a.why = "librccl.so.1 lacks an NCCL entry point";
+  return a;
+}
+
+std::string nccl_err(ncclResult_t r) {
+  return api().error_string ? api().error_string(r) : ("ncclResult " + std::to_string((int)r));
+}
+
+}  // namespace
+
+struct RcclComm {
+  ncclComm_t comm = nullptr;
+  int world = 0, rank = 0;
+};
+
+static_assert(sizeof(ncclUniqueId) == kCommIdBytes, "RCCL unique id size");
+
+int rccl_unique_id(unsigned char *out, std::string &err) {
+  RcclApi &a = api();
+  if (!a.ok) {
+    err = a.why;
+    return -1;
+  }
+  ncclUniqueId id;
+  const ncclResult_t r = a.get_unique_id(&id);
+  if (r != ncclSuccess) {
+    err = "ncclGetUniqueId: " + nccl_err(r);
+    return -1;
+  }
+  memcpy(out, id.internal, kCommIdBytes);
+  return 0;
+}
+
+RcclComm *rccl_init(const unsigned char *id, int world, int rank, std::string &err) {
+  RcclApi &a = api();
+  if (!a.ok) {
+    err = a.why;
+    return nullptr;
+  }
+  ncclUniqueId uid;
+  memcpy(uid.internal, id, kCommIdBytes);
+  RcclComm *c = new RcclComm;
+  c->world = world;
+  c->rank = rank;
+  const ncclResult_t r = a.init_rank(&c->comm, world, uid, rank);  // collective over the world's ranks
+  if (r != ncclSuccess) {
+    err = "ncclCommInitRank: " + nccl_err(r);
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+int rccl_allreduce(RcclComm *c, void *buf, size_t n, bool f64, hipStream_t s, std::string &err) {
+  const ncclResult_t r = api().all_reduce(buf, buf, n, f64 ? ncclFloat64 : ncclUint64, ncclSum, c->comm, s);
+  if (r != ncclSuccess) {
+    err = "ncclAllReduce: " + nccl_err(r);
+    return -1;
+  }
+  return 0;
+}
+
+int rccl_size(const RcclComm *c) { return c ? c->world : 0; }
+
+void rccl_destroy(RcclComm *c) {
+  if (!c) return;
+  if (c->comm) api().destroy(c->comm);
+  delete c;
+}
+
+}  // namespace kml

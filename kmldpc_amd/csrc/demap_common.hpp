@@ -17,12 +17,13 @@ __device__ __forceinline__ double prob_clip(double v) {  // utility.cc:18-26
   return v;
 }
 
-// Quotient n / s from a refined reciprocal r of s (rcp_refine): div2's FAST sequence
-// (bp_common.hpp), bit-identical to an IEEE division when s is normal, n is 0
-// or at least 2^-969, the quotient is normal and the exponent gap is below 768.
-__device__ __forceinline__ double qdiv(double n, double s, double r) {
-  const double m = n * r;
-  return fma(fma(-m, s, n), r, m);
+// FAST quotient n / s with its proof (exact_div.hpp dd_quot / dd_check): ok
+// is cleared when the quotient is not proven correctly rounded, and the caller
+// then reruns the symbol on the exact path.
+__device__ __forceinline__ double qdiv(double n, double s, const DdRcp &r, bool &ok) {
+  const double q = dd_quot(n, r);
+  ok &= dd_check(n, s, q, r);
+  return q;
 }
 
 // Constellation points staged in LDS by the calling kernel (cons_lds); CP is
@@ -66,25 +67,28 @@ __device__ __forceinline__ double exp_core(double x, lds_exptab tab) {
 
 // P0 for the MB bits of one symbol.  FAST: the divisions by var, by the
 // exponential sum, by the prior-weighted sum and by q0 + q1 share one
-// reciprocal refinement each (qdiv); returns false, with out[] unset, when an
-// operand leaves the range where that is exact, and the caller reruns the
-// symbol with IEEE divisions (FAST = false, always true).  The ranges:
-//   * var in [2^-64, 2^64] and every squared distance n_k in [2^-512, 2^512]:
-//     n_k / var is exact (n_k = 0, a symbol exactly on a point, falls back);
+// double-double reciprocal each, and every quotient carries its proof
+// (qdiv, exact_div.hpp); returns false, with out[] unset, when an operand
+// leaves the proof's domain or a quotient is not proven, and the caller reruns
+// the symbol with div_rn (FAST = false, always true).  The domain:
+//   * var in [2^-64, 2^64] and every squared distance n_k in [2^-512, 2^512]
+//     (n_k = 0, a symbol exactly on a point, falls back);
 //   * the exponential sum lies in [1, KC] (its largest term is exp(0) = 1);
-//     a term below 2^-969 divides inexactly, but its quotient and the IEEE one
-//     are both far below 1e-12, so ProbClip maps both to 1e-12;
+//     a term below 2^-969 is outside the proof's domain, but its quotient and
+//     RN's are both far below 1e-12, so ProbClip maps both to 1e-12 whatever
+//     the check says;
 //   * the weighted sum in [2^-64, 2^64] (it is at least w / KC): the clipped
-//     terms (>= w * 1e-12) divide exactly, and so do q0 and q1 (>= 1e-14,
-//     q0 + q1 ~ 2).
+//     terms (>= w * 1e-12) and q0, q1 (>= 1e-14, q0 + q1 ~ 2) are inside.
 template <int MB, bool FAST, class CP>
 __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double yr, double yi, double hr,
                                                double hi, double var, double *out) {
   constexpr int KC = 1 << MB;
   double pr[KC];
   double mx = 0.0;
-  double nmin = 0.0, nmax = 0.0, rv = 0.0;
-  if (FAST) rv = rcp_refine(var);
+  double nmin = 0.0, nmax = 0.0;
+  bool dok = true;  // every FAST quotient proven correctly rounded
+  DdRcp rv{};
+  if (FAST) rv = dd_rcp(var);
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
     const double cr = cons[2 * k], ci = cons[2 * k + 1];
@@ -97,14 +101,14 @@ __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double 
     if (FAST) {
       nmin = k == 0 ? n : fmin(nmin, n);
       nmax = k == 0 ? n : fmax(nmax, n);
-      d = qdiv(n, var, rv);
+      d = qdiv(n, var, rv, dok);
     } else {
-      d = n / var;
+      d = div_rn(n, var);
     }
     pr[k] = -d;
     if (k == 0 || mx < pr[k]) mx = pr[k];  // *max_element
   }
-  if (FAST && !(nmin >= 0x1p-512 && nmax <= 0x1p512 && var >= 0x1p-64 && var <= 0x1p64)) return false;
+  if (FAST && !(dok && nmin >= 0x1p-512 && nmax <= 0x1p512 && var >= 0x1p-64 && var <= 0x1p64)) return false;
   double sum = 0.0;
   bool eok = true;
 #pragma unroll
@@ -123,18 +127,25 @@ __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double 
   double w = 1.0;  // prod over bits of bitLin (= 0.5) or 1 - bitLin (= 0.5)
 #pragma unroll
   for (int j = 0; j < MB; ++j) w *= 0.5;
-  const double rs = FAST ? rcp_refine(sum) : 0.0;
+  DdRcp rs{};
+  if (FAST) rs = dd_rcp(sum);
   double sum2 = 0.0;
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
-    pr[k] = prob_clip(prob_clip(FAST ? qdiv(pr[k], sum, rs) : pr[k] / sum));
+    bool ok_k = true;
+    const double qk = FAST ? qdiv(pr[k], sum, rs, ok_k) : div_rn(pr[k], sum);
+    // a faithful quotient below 1e-12 has RN's clip: RN is it or its upper
+    // neighbour, at most 1e-12 (terms below 2^-969, outside the check's domain)
+    if (FAST) dok &= ok_k | (qk < kSmallestProb);
+    pr[k] = prob_clip(prob_clip(qk));
     pr[k] = w * pr[k];
     sum2 += pr[k];
   }
-  if (FAST && !(sum2 >= 0x1p-64 && sum2 <= 0x1p64)) return false;
-  const double rs2 = FAST ? rcp_refine(sum2) : 0.0;
+  if (FAST && !(dok && sum2 >= 0x1p-64 && sum2 <= 0x1p64)) return false;
+  DdRcp rs2{};
+  if (FAST) rs2 = dd_rcp(sum2);
 #pragma unroll
-  for (int k = 0; k < KC; ++k) pr[k] = FAST ? qdiv(pr[k], sum2, rs2) : pr[k] / sum2;
+  for (int k = 0; k < KC; ++k) pr[k] = FAST ? qdiv(pr[k], sum2, rs2, dok) : div_rn(pr[k], sum2);
   // per-bit sums in ascending k (modem.cc:58-70); one bit at a time keeps two
   // accumulators live next to the KC probabilities
 #pragma unroll
@@ -150,9 +161,14 @@ __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double 
     q0 /= 0.5;
     q1 /= (1.0 - 0.5);
     const double t = q0 + q1;
-    out[j] = prob_clip(FAST ? qdiv(q0, t, rcp_refine(t)) : q0 / t);
+    if constexpr (FAST) {
+      const DdRcp rt = dd_rcp(t);
+      out[j] = prob_clip(qdiv(q0, t, rt, dok));
+    } else {
+      out[j] = prob_clip(div_rn(q0, t));
+    }
   }
-  return true;
+  return dok;
 }
 
 template <int MB, class CP>

@@ -1,0 +1,168 @@
+// exact_div.hpp — correctly rounded double division on gfx950.
+//
+// The reference divides with x86-64 `divsd`: RN(n / s) for every operand pair.
+// gfx950 has no f64 divide instruction, and hipcc's f64 '/' (v_div_scale,
+// v_rcp_f64, two Newton steps, the Markstein tail, v_div_fmas, v_div_fixup) is
+// NOT correctly rounded everywhere: its refined reciprocal is one ulp low for
+// s = 1 - k 2^-53 (k = 3, 5, ..., 13), and e.g. 0x1.6666666666663p-1 /
+// 0x1.ffffffffffffbp-1 comes out one ulp low (tools/probe/cn_div_candidates.py,
+// tests/test_gpu_parity.py::test_exact_division_*).  Everything here is
+// provably RN(n / s).
+//
+// 1. dd_quot + dd_check (the decoders' FAST VN divisions, demap_common.hpp):
+//    y1 = v_rcp_f64(s) after one Newton step, e1 = 1 - s y1 (exact: fma),
+//    ylo = RN(e1 y1).  y1 + e1 y1 = (1 - e1^2) / s, so
+//        q = fma(n, y1, RN(n ylo))
+//    rounds n/s (1 - e1^2) + O(n/s |e1| 2^-53) once: |e1| <= 2^-52 + eps0^2
+//    (eps0 = the relative error of v_rcp_f64, far below 2^-14 on gfx950), so the
+//    value rounded is within 2^-50 ulp of n/s and q is a FAITHFUL rounding of
+//    n/s (one of its two neighbours), correctly rounded except when n/s lies
+//    within 2^-50 ulp of a rounding midpoint.
+//    The check: r = fma(-q, s, n) is exact (q faithful; n = 0 or n >= 2^-969,
+//    s and q normal), and with k = y1 (1 + 2^-30) >= (1 + 2^-31) / s
+//    (|1 - s y1| = |e1| <= 2^-51), r k = (n/s - q)(1 + kappa) exactly inside
+//        t = fma(r, k, q) = RN(q + (n/s - q) (1 + kappa)),  2^-31 <= kappa <= 2^-29
+//    (the default form t = fma(RN(r (1 + 2^-30)), y1, q) has the same bound:
+//    the extra rounding multiplies 1 + kappa by 1 + delta, |delta| <= 2^-53).
+//    If q != RN(n/s), |n/s - q| exceeds half the gap g between q and its
+//    neighbour towards n/s (g = ulp(q), or ulp(q)/2 below a power of two; n/s
+//    is never exactly a midpoint: s times a 54-bit odd significand has more
+//    than 53 bits), so q + (n/s - q)(1 + kappa) lies beyond that midpoint and
+//    t != q.  Contrapositive: t == q proves q == RN(n/s).  A correct q is
+//    flagged only when n/s lies within ~2^-30 ulp of a midpoint (probability
+//    ~2^-29 per quotient); the caller then redoes the work with div_rn.
+//    Cost per normalisation pair: 6 shared + 5 per quotient (the unchecked
+//    hipcc-sequence form was 5 + 3).
+//
+// 2. div_rn (every other division: the decoders' exact re-decode, the
+//    non-FAST demap, k-means): any operands.  Finite normal operands with
+//    2^-969 <= |n| < 2^1000, 2^-1000 <= |s| < 2^1000 and a normal quotient:
+//    q from dd_quot (faithful, above), r = fma(-q, s, n) exact, and q is
+//    replaced by its neighbour qn towards n/s when |fma(-qn, s, n)| < |r|
+//    (both residuals exact, |residual| = |s| * distance to n/s; no ties).
+//    Zeros, infinities and NaNs: hipcc's '/' (its special-case handling is
+//    IEEE-754's, and the NaN payloads are the ones the parity tests pinned).
+//    Other finite nonzero operands (subnormal or extreme): div_soft, an
+//    integer long division of the significands with round-to-nearest-even
+//    onto the normal or subnormal grid.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace kml {
+
+// KML_DD_CHECK_K (A/B): 1 = k = y1 (1 + 2^-30) kept per reciprocal (one mul
+// per pair, two more live registers per pair in flight); 0 = the residual
+// scaled by 1 + 2^-30 per quotient (one mul per quotient, no register).  The
+// same proof: r (1 + 2^-30) y1 = (n/s - q)(1 + 2^-30) s y1.
+#ifndef KML_DD_CHECK_K
+#define KML_DD_CHECK_K 0
+#endif
+struct DdRcp {
+  double hi, lo;  // y1, RN(e1 y1)
+#if KML_DD_CHECK_K
+  double k;  // y1 (1 + 2^-30)
+#endif
+};
+
+__device__ __forceinline__ DdRcp dd_rcp(double s) {
+  const double y0 = __builtin_amdgcn_rcp(s);
+  const double y1 = fma(y0, fma(-y0, s, 1.0), y0);
+  const double e1 = fma(-y1, s, 1.0);
+#if KML_DD_CHECK_K
+  return {y1, e1 * y1, y1 * (1.0 + 0x1p-30)};
+#else
+  return {y1, e1 * y1};
+#endif
+}
+
+__device__ __forceinline__ double dd_quot(double n, const DdRcp &y) { return fma(n, y.hi, n * y.lo); }
+
+// true when q == RN(n / s) is proven (see 1. above)
+__device__ __forceinline__ bool dd_check(double n, double s, double q, const DdRcp &y) {
+#if KML_DD_CHECK_K
+  return fma(fma(-q, s, n), y.k, q) == q;
+#else
+  return fma(fma(-q, s, n) * (1.0 + 0x1p-30), y.hi, q) == q;
+#endif
+}
+
+// Integer long division for finite nonzero n, s (any magnitude): RN(n / s).
+__device__ __forceinline__ double div_soft(double n, double s) {
+  const uint64_t bn = (uint64_t)__double_as_longlong(n), bs = (uint64_t)__double_as_longlong(s);
+  const uint64_t sign = (bn ^ bs) & 0x8000000000000000ull;
+  constexpr uint64_t kMant = (1ull << 52) - 1;
+  int en = (int)((bn >> 52) & 0x7FF), es = (int)((bs >> 52) & 0x7FF);
+  uint64_t mn = bn & kMant, ms = bs & kMant;
+  // value = m * 2^(e - 1075) with m in [2^52, 2^53) after normalisation
+  if (en) mn |= 1ull << 52; else en = 1;
+  if (es) ms |= 1ull << 52; else es = 1;
+  {
+    const int zn = __clzll((long long)mn) - 11, zs = __clzll((long long)ms) - 11;
+    mn <<= zn;
+    en -= zn;
+    ms <<= zs;
+    es -= zs;
+  }
+  int e = en - es;  // n / s = (mn / ms) 2^e
+  if (mn < ms) {
+    mn <<= 1;
+    --e;
+  }
+  // Q = floor((mn / ms) 2^53) in [2^53, 2^54), sticky = remainder != 0
+  uint64_t Q = 0, rem = mn;
+  for (int i = 0; i < 54; ++i) {
+    const bool ge = rem >= ms;
+    Q = (Q << 1) | (ge ? 1ull : 0ull);
+    if (ge) rem -= ms;
+    rem <<= 1;
+  }
+  const bool sticky = rem != 0;
+  uint64_t out;
+  if (e >= -1022) {  // normal: significand Q >> 1, round bit Q & 1
+    uint64_t S = Q >> 1;
+    if ((Q & 1) && (sticky || (S & 1))) ++S;
+    if (S >> 53) {
+      S >>= 1;
+      ++e;
+    }
+    if (e > 1023) return __longlong_as_double((long long)(sign | 0x7FF0000000000000ull));
+    out = ((uint64_t)(e + 1023) << 52) | (S & kMant);
+  } else {  // subnormal grid 2^-1074: N = (mn / ms) 2^(e + 1074) = Q 2^(e + 1021)
+    const int sh = -(e + 1021);  // >= 2
+    if (sh > 55) {
+      out = 0;  // below half the smallest subnormal
+    } else {
+      const uint64_t N = Q >> sh;
+      const bool rbit = (Q >> (sh - 1)) & 1;
+      const bool st = sticky || (Q & ((1ull << (sh - 1)) - 1)) != 0;
+      out = N + ((rbit && (st || (N & 1))) ? 1 : 0);  // may carry into the smallest normal
+    }
+  }
+  return __longlong_as_double((long long)(sign | out));
+}
+
+// RN(n / s) for any operands (see 2. above).
+__device__ __forceinline__ double div_rn(double n, double s) {
+  const double an = fabs(n), as = fabs(s);
+  if (an >= 0x1p-969 && an < 0x1p1000 && as >= 0x1p-1000 && as < 0x1p1000) {
+    const DdRcp y = dd_rcp(s);
+    double q = dd_quot(n, y);
+    const double aq = fabs(q);
+    if (aq >= 0x1p-1020 && aq < 0x1p1020) {
+      const double r = fma(-q, s, n);
+      if (r != 0.0) {
+        // the neighbour of q towards n / s (whose sign is r's times s's)
+        const long long step = ((r > 0.0) == (s > 0.0)) == (q > 0.0) ? 1 : -1;
+        const double qn = __longlong_as_double(__double_as_longlong(q) + step);
+        if (fabs(fma(-qn, s, n)) < fabs(r)) q = qn;
+      }
+      return q;
+    }
+  }
+  if (!(an > 0.0) || !(as > 0.0) || an == INFINITY || as == INFINITY) return n / s;  // 0, inf, NaN: IEEE cases
+  return div_soft(n, s);
+}
+
+}  // namespace kml

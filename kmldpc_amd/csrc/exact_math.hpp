@@ -33,8 +33,11 @@
 //                reached only when both parts are NaN.
 //
 // Everything here uses only IEEE-754 basic operations and sqrt, which are
-// correctly rounded on gfx950 and on x86-64, so host and device produce the
-// same bits.  Compile with -ffp-contract=off.
+// correctly rounded on x86-64 and, on gfx950, through kml_div (division;
+// hipcc's '/' is not correctly rounded everywhere, exact_div.hpp) and the
+// hardware's add/mul/fma/sqrt, so host and device produce the same bits.
+// Divisions by powers of two are exact either way and keep '/'.  Compile
+// with -ffp-contract=off.
 #pragma once
 
 #if defined(__HIPCC__)
@@ -49,8 +52,21 @@
 
 #include "exp_table.hpp"
 #include "log_table.hpp"
+#if defined(__HIPCC__)
+#include "exact_div.hpp"
+#endif
 
 namespace kml {
+
+// RN(a / b): the host's IEEE division, and on the device exact_div.hpp div_rn
+// (hipcc's f64 '/' is not correctly rounded everywhere).
+KML_HD double kml_div(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return div_rn(a, b);
+#else
+  return a / b;
+#endif
+}
 
 struct cplx {
   double re, im;
@@ -69,7 +85,7 @@ KML_HD double hypot_kernel(double ax, double ay) {
     t1 = 2.0 * delta * (ax - 2.0 * ay);
     t2 = (4.0 * delta - ay) * ay + delta * delta;
   }
-  h -= (t1 + t2) / (2.0 * h);
+  h -= kml_div(t1 + t2, 2.0 * h);
   return h;
 }
 
@@ -103,24 +119,24 @@ KML_HD cplx kml_cdiv(cplx n, cplx dd) {
   const double RMIN = 2.2250738585072014e-308;  // DBL_MIN
   double denom, ratio, x, y;
   if (fabs(c) < fabs(d)) {
-    ratio = c / d;
+    ratio = kml_div(c, d);
     denom = (c * ratio) + d;
     if (fabs(ratio) > RMIN) {
-      x = ((a * ratio) + b) / denom;
-      y = ((b * ratio) - a) / denom;
+      x = kml_div((a * ratio) + b, denom);
+      y = kml_div((b * ratio) - a, denom);
     } else {
-      x = ((c * (a / d)) + b) / denom;
-      y = ((c * (b / d)) - a) / denom;
+      x = kml_div((c * kml_div(a, d)) + b, denom);
+      y = kml_div((c * kml_div(b, d)) - a, denom);
     }
   } else {
-    ratio = d / c;
+    ratio = kml_div(d, c);
     denom = (d * ratio) + c;
     if (fabs(ratio) > RMIN) {
-      x = ((b * ratio) + a) / denom;
-      y = (b - (a * ratio)) / denom;
+      x = kml_div((b * ratio) + a, denom);
+      y = kml_div(b - (a * ratio), denom);
     } else {
-      x = (a + (d * (b / c))) / denom;
-      y = (b - (d * (a / c))) / denom;
+      x = kml_div(a + (d * kml_div(b, c)), denom);
+      y = kml_div(b - (d * kml_div(a, c)), denom);
     }
   }
   // C99 Annex G recovery of infinities and zeros (what __divdc3 does when

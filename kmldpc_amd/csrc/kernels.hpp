@@ -49,6 +49,7 @@ enum {
   CNT_VN_PHASES = 4,
   CNT_CN_PHASES = 5,
   CNT_CONVERGED = 6,
+  CNT_REDONE = 7,  // FAST decodes redone on the exact path (an unproven quotient, exact_div.hpp)
   CNT_N = 8
 };
 
@@ -98,6 +99,11 @@ struct BpLaunch {
   int sym_bits = 0;
 };
 
+// FAST-path mode of a BP launch: bit 0 = FAST division allowed (column degree
+// <= kFastMaxColumnDegree, and not KML_NO_FAST=1: every codeword on the
+// exact path); bit 1 = KML_FORCE_REDO=1 (tests: every FAST decode is treated
+// as suspect and redone on the exact path, exercising the redo machinery).
+int bp_fast_mode(const DevCode &c);
 hipError_t launch_bp_regular(const DevCode &c, const BpLaunch &a, hipStream_t s);
 // Can the regular kernel compute P0 itself (BpLaunch::sym_y) for this code and modem?
 bool bp_regular_fuses_demap(const DevCode &c, int bits);

@@ -644,7 +644,7 @@ __device__ KM_SLOW cplx cdiv_slow(cplx n, cplx dd) { return kml_cdiv(n, dd); }
 // signed zeros).  Anything else takes the full restatement.
 __device__ __forceinline__ cplx cdiv_count(double a, double b, int cnt) {
   const double c = (double)cnt;
-  if (cnt > 0 && a != 0.0 && b != 0.0 && isfinite(a) && isfinite(b)) return cplx{a / c, b / c};
+  if (cnt > 0 && a != 0.0 && b != 0.0 && isfinite(a) && isfinite(b)) return cplx{kml_div(a, c), kml_div(b, c)};
   return cdiv_slow(cplx{a, b}, cplx{c, 0.0});
 }
 
@@ -659,11 +659,11 @@ __device__ __forceinline__ CdivConst cdiv_prepare(cplx dd) {
   const double c = dd.re, d = dd.im;
   CdivConst k;
   if (fabs(c) < fabs(d)) {
-    k.ratio = c / d;
+    k.ratio = kml_div(c, d);
     k.denom = (c * k.ratio) + d;
     k.mode = 1;
   } else {
-    k.ratio = d / c;
+    k.ratio = kml_div(d, c);
     k.denom = (d * k.ratio) + c;
     k.mode = 2;
   }
@@ -673,11 +673,11 @@ __device__ __forceinline__ CdivConst cdiv_prepare(cplx dd) {
 __device__ __forceinline__ cplx cdiv_const(cplx n, cplx dd, const CdivConst &k) {
   double x, y;
   if (k.mode == 1) {
-    x = ((n.re * k.ratio) + n.im) / k.denom;
-    y = ((n.im * k.ratio) - n.re) / k.denom;
+    x = kml_div((n.re * k.ratio) + n.im, k.denom);
+    y = kml_div((n.im * k.ratio) - n.re, k.denom);
   } else if (k.mode == 2) {
-    x = ((n.im * k.ratio) + n.re) / k.denom;
-    y = (n.im - (n.re * k.ratio)) / k.denom;
+    x = kml_div((n.im * k.ratio) + n.re, k.denom);
+    y = kml_div(n.im - (n.re * k.ratio), k.denom);
   } else {
     return cdiv_slow(n, dd);
   }
@@ -1119,19 +1119,24 @@ __global__ void div_probe_kernel(const double *in, int n, double *out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double n0 = in[3 * i], n1 = in[3 * i + 1], s = in[3 * i + 2];
-  double q0, q1, r0, r1, c0, c1;
-  div2<true>(n0, n1, s, q0, q1);
-  div2<false>(n0, n1, s, r0, r1);
+  double q0, q1, c0, c1;
+  bool sus = false;
+  div2<true>(n0, n1, s, q0, q1, sus);  // the FAST VN form: dd_quot + dd_check
+  const DdRcp y = dd_rcp(s);
+  const int flags = (dd_check(n0, s, q0, y) ? 0 : 1) | (dd_check(n1, s, q1, y) ? 0 : 2);
   div2<true, true>(n0, n1, s, c0, c1);
-  double *o = out + 8 * (long long)i;
+  double *o = out + 11 * (long long)i;
   o[0] = q0;
   o[1] = q1;
-  o[2] = r0;
-  o[3] = r1;
+  o[2] = div_rn(n0, s);
+  o[3] = div_rn(n1, s);
   o[4] = c0;
   o[5] = c1;
   o[6] = rcp_near1(s);
   o[7] = rcp_refine(s);
+  o[8] = n0 / s;  // hipcc's '/'
+  o[9] = n1 / s;
+  o[10] = (double)(flags | (sus ? 4 : 0));
 }
 }  // namespace
 

@@ -75,7 +75,7 @@ def point_seed(seed, i):
 class Simulator:
     """Simulator (include/simulator.h): constructed from config.toml, Simulate() runs the sweep."""
 
-    def __init__(self, config, data_dir=None, device=0, batch=32768, seed=0, dist=None, log=None):
+    def __init__(self, config, data_dir=None, device=0, batch=32768, seed=0, dist=None, log=None, comm_backend="nccl"):
         self.ctx = Context(config, data_dir=data_dir or os.path.dirname(os.path.abspath(config)), device=device)
         self.rc = self.ctx.run_config()
         self.batch = int(batch)
@@ -84,17 +84,23 @@ class Simulator:
         self.rank = dist.get_rank() if dist else 0
         self.world = dist.get_world_size() if dist else 1
         self.log = log or Logger(enabled=self.rank == 0)
+        if dist is not None and comm_backend == "nccl":  # RCCL communicator for the counter all-reduces
+            from . import comm_unique_id
+            uid = [comm_unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            self.ctx.comm_init(uid[0], self.world, self.rank)
         rc = self.rc
         self.log.info("Using 5G LDPC." if rc["5gldpc"] else "Using traditional LDPC.")
         self.log.info(f"[{rc['minimum_snr']:.3f},{rc['step_snr']:.3f},{rc['maximum_snr']:.3f}]")
         self.log.info(f"[MAX_ERROR_BLK = {rc['maximum_error_number']},MAX_BLK = {rc['maximum_block_number']}]")
 
     def _reduce(self, a):
+        if self.ctx.comm_size():  # the library's RCCL communicator (xGMI), on the context's stream
+            return self.ctx.comm_allreduce(np.ascontiguousarray(a, np.uint64))
         import torch
-        dev = "cuda" if self.dist.get_backend() == "nccl" else "cpu"
-        t = torch.from_numpy(a.astype(np.int64)).to(dev)
-        self.dist.all_reduce(t)
-        return t.cpu().numpy().astype(np.uint64)
+        t = torch.from_numpy(a.astype(np.int64))
+        self.dist.all_reduce(t)  # gloo
+        return t.numpy().astype(np.uint64)
 
     def run(self, snr, i):
         """Simulator::run for one SNR point -> (ber, fer, counters)."""
@@ -153,16 +159,16 @@ def main(argv=None):
     lib()  # the HIP library (and its ROCm runtime) before torch
     dist = None
     if world > 1 or (args.force_dist and "WORLD_SIZE" in os.environ):
-        import torch
+        # gloo: rendezvous and CPU control; the counters' all-reduce is the
+        # library's own RCCL communicator with --dist-backend nccl (see bench.py)
         import torch.distributed as dist_mod
-        if args.dist_backend == "nccl":
-            torch.cuda.set_device(local)
-            dist_mod.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-        else:
+        dist_mod.init_process_group(backend="gloo")
+        if args.dist_backend != "nccl":  # gloo counters: ranks may share a GPU
+            import torch
             local = local % max(torch.cuda.device_count(), 1)
-            dist_mod.init_process_group(backend="gloo")
         dist = dist_mod
-    sim = Simulator(args.config, device=local, batch=args.batch, seed=args.seed, dist=dist, log=log)
+    sim = Simulator(args.config, device=local, batch=args.batch, seed=args.seed, dist=dist, log=log,
+                    comm_backend=args.dist_backend)
     sim.Simulate()
     sim.ctx.close()
     if dist is not None:

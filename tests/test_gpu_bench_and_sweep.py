@@ -157,7 +157,7 @@ def test_bench_two_ranks_gloo(data_dir, tmp_path):
     B = 2048
     line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--steps", "2", "--warmup", "1", "--batch", str(B),
                    "--no-cpu-baseline", "--no-ber-match", "--full-loop-batches", "1"])
-    assert line["n_gpus"] == 2 and line["ranks"] == 2 and line["dist_backend"] == "gloo"
+    assert line["n_gpus"] == 2 and line["ranks"] == 2 and line["dist_backend"].startswith("gloo counters")
     assert len(line["rank_ms_per_step"]) == 2 and line["config"]["global_batch"] == 2 * B
     st = line["stats"]
     assert st["codewords"] == 2 * B
@@ -172,15 +172,15 @@ def test_bench_two_ranks_gloo(data_dir, tmp_path):
 
 def test_bench_one_rank_rccl_group(data_dir):
     """The RCCL leg on hardware: `bench.py --gpus 1 --force-dist` runs one rank
-    under torch.distributed.run with a 1-rank NCCL (= RCCL) process group —
-    init_process_group(nccl, device_id), the cuda-tensor all_reduce of the
-    counters and the all_gather of the rank times — and its counters equal the
-    plain single-process run on the same frames."""
+    under torch.distributed.run (gloo rendezvous), builds the library's RCCL
+    communicator (kml_comm_unique_id / kml_comm_init) and all-reduces the
+    counters through it (kml_comm_allreduce_f64, on the context's stream); its
+    counters equal the plain single-process run on the same frames."""
     args = ["--steps", "2", "--warmup", "1", "--batch", "2048", "--no-cpu-baseline", "--no-ber-match",
             "--full-loop-batches", "1"]
     plain = _bench(args)
     line = _bench(args + ["--gpus", "1", "--force-dist"])
-    assert line["rccl_ranks"] == 1 and line["dist_backend"] == "nccl" and line["ranks"] == 1
+    assert line["rccl_ranks"] == 1 and line["dist_backend"].startswith("rccl counters") and line["ranks"] == 1
     assert len(line["rank_ms_per_step"]) == 1
     for k in ("fer", "ber", "codewords", "mean_cn_phases"):
         assert line["stats"][k] == plain["stats"][k], k
@@ -188,9 +188,10 @@ def test_bench_one_rank_rccl_group(data_dir):
 
 def test_simulate_one_rank_rccl_group(data_dir, tmp_path):
     """kmldpc_amd.simulate under torchrun --nproc-per-node 1 with a forced
-    1-rank NCCL group (KML_FORCE_DIST=1): the per-round stop-rule and counter
-    all-reduces run on cuda tensors through RCCL, and the BER / FER tables equal
-    the run without a process group."""
+    1-rank process group (KML_FORCE_DIST=1, --dist-backend nccl): the
+    per-round stop-rule and counter all-reduces of kml_sim_point run through
+    the library's RCCL communicator, and the BER / FER tables equal the run
+    without a process group."""
     cfg = tmp_path / "config.toml"
     write_config(str(cfg), data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", known=False, snr=1.0, snr_max=2.0,
                  snr_step=1.0, max_blocks=3000, max_err=700, thread_blocks=1000)

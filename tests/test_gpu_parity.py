@@ -106,12 +106,22 @@ def test_device_exp_vs_glibc(data_dir):
     assert np.array_equal(out, ref)
 
 
-def test_fast_division_is_ieee_exact(data_dir):
-    """The decoder's shared-reciprocal division pair (bp_common.hpp div2) equals
-    two IEEE divisions over the value domain it is used on: numerators in
-    {0} U [2^-840, 1], s = n0 + n1 (the normalisations of the BP chains)."""
+def _same(a, b):
+    """bitwise equality, any NaN equal to any NaN"""
+    return (a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
+
+
+def test_fast_division_proven_or_flagged(data_dir):
+    """The decoder's FAST VN division (exact_div.hpp dd_quot + dd_check, used
+    by bp_common.hpp div2) over the value domain it runs on: numerators in
+    {0} U [2^-840, 1], s = RN(n0 + n1) (the normalisations of the BP chains).
+    Every quotient the check passes equals IEEE division; the check flags a
+    quotient only near a rounding midpoint (the decoder then redoes the
+    codeword on the exact path), which random operands almost never are; and
+    div_rn equals IEEE division on all of them."""
     ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
     rng = np.random.default_rng(7)
+    flagged = total = 0
     for scale_exp in (1, 8, 40, 200, 840):
         n = 400000
         n0 = rng.random(n) * 2.0 ** -rng.uniform(0, scale_exp, n)
@@ -124,9 +134,43 @@ def test_fast_division_is_ieee_exact(data_dir):
         keep = s > 0
         x = np.stack([n0[keep], n1[keep], s[keep]], axis=1)
         out = ctx.div_probe(x)
-        assert np.array_equal(out[:, 2], x[:, 0] / x[:, 2])  # device IEEE == numpy IEEE
-        assert np.array_equal(out[:, 0], out[:, 2]), scale_exp
-        assert np.array_equal(out[:, 1], out[:, 3]), scale_exp
+        ref0, ref1 = x[:, 0] / x[:, 2], x[:, 1] / x[:, 2]
+        f = out[:, 10].astype(np.int64)
+        assert np.array_equal(out[f & 1 == 0, 0], ref0[f & 1 == 0]), scale_exp
+        assert np.array_equal(out[f & 2 == 0, 1], ref1[f & 2 == 0]), scale_exp
+        assert np.array_equal((f & 4) != 0, (f & 3) != 0)  # div2's suspect flag is the OR of the two
+        assert np.array_equal(out[:, 2], ref0) and np.array_equal(out[:, 3], ref1), scale_exp  # div_rn
+        flagged += int(np.count_nonzero(f & 3))
+        total += 2 * x.shape[0]
+    print(f"FAST quotients flagged: {flagged} of {total}")
+    assert flagged <= total * 1e-6
+
+
+def test_exact_division_any_operands(data_dir):
+    """div_rn (exact_div.hpp: every division off the FAST path, the demapper's
+    and k-means') equals x86 IEEE division bit for bit on any operands: every
+    exponent incl. subnormal and overflowing quotients, signs, zeros,
+    infinities and NaN (NaN equal to NaN)."""
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    rng = np.random.default_rng(11)
+    n = 600000
+    a = (rng.random(n) + 0.5) * 2.0 ** rng.integers(-1074, 1024, n).astype(np.float64)
+    b = (rng.random(n) + 0.5) * 2.0 ** rng.integers(-1074, 1024, n).astype(np.float64)
+    a *= np.where(rng.random(n) < 0.5, -1.0, 1.0)
+    bits = rng.integers(0, 2 ** 63, n, dtype=np.int64)  # raw patterns: subnormals, NaNs, infinities
+    a[::7] = bits[::7].view(np.float64)
+    b[3::11] = bits[3::11][::-1].view(np.float64)
+    special = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -5e-324, 2.2250738585072014e-308,
+                        1.7976931348623157e308, 1.0, -1.0, 3.0])
+    sa, sb = np.meshgrid(special, special)
+    a = np.concatenate([a, sa.ravel()])
+    b = np.concatenate([b, sb.ravel()])
+    x = np.stack([a, a, b], axis=1)
+    out = ctx.div_probe(x)
+    with np.errstate(all="ignore"):
+        ref = a / b
+    bad = ~_same(out[:, 2], ref)
+    assert not bad.any(), (a[bad][:4], b[bad][:4], out[bad, 2][:4], ref[bad][:4])
 
 
 def _near_midpoint_significands(K, width):
@@ -178,7 +222,13 @@ def test_cn_reciprocal_exhaustive(data_dir):
     out = ctx.div_probe(x)
     ref = x[:, 0] / x[:, 2]
     assert np.array_equal(out[:, 4], ref)
-    print(f"near-midpoint candidates: {len(rows)}; hipcc '/' misrounds {int(np.sum(out[:, 2] != ref))}")
+    assert np.array_equal(out[:, 2], ref)  # div_rn
+    f = out[:, 10].astype(np.int64)
+    assert np.array_equal(out[f & 1 == 0, 0], ref[f & 1 == 0])  # the FAST VN form: proven, or flagged
+    miss = int(np.sum(out[:, 8] != ref))
+    print(f"near-midpoint candidates: {len(rows)}; hipcc '/' misrounds {miss}; "
+          f"FAST VN form flags {int(np.count_nonzero(f & 1))}")
+    assert miss > 0  # the finding that motivates exact_div.hpp (hipcc's '/' is not RN everywhere)
     # random normalisation-like pairs (products of normalised pairs), the CN
     # phases' operands (their sums are within 2^-49 of 1: bp_common.hpp rcp_cn_rows)
     n = 400000
@@ -739,3 +789,58 @@ def test_chunked_decode_reports_abort_of_an_early_chunk(data_dir, blind, monkeyp
     r1 = ctx.decode_frames(y, 6.0, None if blind else th)  # the abort was reported and cleared
     for k in ("uu_hat", "ret"):
         assert np.array_equal(r1[k], r0[k]), k
+
+
+# The exact path and the redo machinery (exact_div.hpp, DESIGN.md "Exact
+# division"): KML_NO_FAST=1 decodes every codeword on the exact path (div_rn
+# everywhere); KML_FORCE_REDO=1 treats every FAST decode as suspect, so each
+# codeword is decoded on the FAST path, deferred at its first CN barrier and
+# redone by the exact kernel (regular / irregular: the second launch; the
+# partitioned kernel: tagged -> barrier-exchange FAST -> exact).  Both must
+# reproduce the reference bit for bit, syndromes included.
+EXACT_MODES = ["KML_NO_FAST", "KML_FORCE_REDO"]
+
+
+@pytest.mark.parametrize("mode", EXACT_MODES)
+@pytest.mark.parametrize("case", ["peg2304_qpsk_known", "bg2_16qam_known", "peg8064_64qam_known",
+                                  "peg2304_4psk_known_lowsnr"])
+def test_exact_path_golden_vectors(case, data_dir, mode, monkeypatch):
+    hdr, z = load_case(case)
+    monkeypatch.setenv(mode, "1")
+    ctx = ctx_for(data_dir, hdr["matrix"], hdr["modem"], bool(hdr["is5g"]), hdr["max_iter"])
+    p0 = z["v_p0"]
+    B = p0.shape[0]
+    syn0 = np.full((B, ctx.M), -1.0)
+    r = ctx.bp_decode(p0, cc_hat=True, syn=syn0)
+    assert np.array_equal(r["ret"], z["s_ret"][:B])
+    assert np.array_equal(r["uu_hat"], z["v_uu_hat"])
+    assert np.array_equal(r["cc_hat"], z["v_cc_hat"])
+    for i in range(B):
+        if r["ret"][i] > 1:
+            assert np.array_equal(r["syn"][i], z["v_syn"][i]), f"syndrom_soft cw {i}"
+        else:  # no CN phase ran: the rows the caller passed in stay (the reference's member array)
+            assert np.array_equal(r["syn"][i], syn0[i]), f"syndrom_soft cw {i} written without a CN phase"
+
+
+@pytest.mark.parametrize("mode", EXACT_MODES)
+@pytest.mark.parametrize("case", ["peg2304_qpsk_known", "peg2304_qpsk_blind", "bg2_16qam_blind", "peg8064_64qam_blind"])
+def test_exact_path_reference_stream(case, data_dir, mode, monkeypatch):
+    """KmCodec::Decoder on the reference's frames through the exact path and
+    through forced redos (fused QPSK demap prologue included): chosen
+    candidate, return values and decoded bits equal the reference's."""
+    monkeypatch.setenv(mode, "1")
+    test_decode_frames_vs_reference_stream(case, data_dir)
+
+
+def test_forced_redo_counts_and_counters(data_dir, monkeypatch):
+    """Every FAST decode of a forced-redo run is counted as redone (and once
+    only), and the sim path's counters equal the normal run's."""
+    ctx = ctx_for(data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", False)
+    ctx.sim_generate(2.0, 1024, seed=5, first_cw=0)
+    c0 = ctx.sim_decode(2.0, blind=False)
+    assert c0["redone"] <= 2  # ~2^-29 per quotient: none expected at this size
+    monkeypatch.setenv("KML_FORCE_REDO", "1")
+    c1 = ctx.sim_decode(2.0, blind=False)
+    assert c1["redone"] == 1024
+    for k in ("err_bit", "err_blk", "tot_bit", "tot_blk", "vn_phases", "cn_phases", "converged"):
+        assert c1[k] == c0[k], k

@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU session: optionally the GPU tests ($TESTS=1, $TESTS_K a -k filter),
+# then bench lines of several library builds for several workloads, two rounds
+# each, interleaved (same box).  $LIBS: kmldpc_amd/libkmldpc_amd_<x>.so
+# suffixes ("main" = the product build); $WORKLOADS: headline blind bg2 peg8064.
+# Outputs under gpurun_out/$1/; every GPU step under its own time limit.
+set -o pipefail
+O=gpurun_out/${1:-ab}; mkdir -p $O
+if [ "${TESTS:-0}" = 1 ]; then
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${TESTS_K:+-k "$TESTS_K"} > $O/gpu_tests.log 2>&1 || exit $?
+fi
+for r in 1 2; do
+  for w in ${WORKLOADS:-headline}; do
+    case $w in
+      headline) A="" ;;
+      blind) A="--blind" ;;
+      bg2) A="--matrix 5GLDPCBG2a3_R12_K960.txt --modem 4bit_16QAM_Gray.txt --is5g --snr 5.01 --max-iter 50 --batch 16384 --steps 5" ;;
+      peg8064) A="--matrix PEG8064regular0.5.txt --modem 6bits_64QAM_Gray.txt --snr 6.77 --blind --batch 4096 --steps 3" ;;
+      *) echo "unknown workload $w"; exit 2 ;;
+    esac
+    for l in ${LIBS:-main}; do
+      if [ "$l" = main ]; then L=kmldpc_amd/libkmldpc_amd.so; else L=kmldpc_amd/libkmldpc_amd_$l.so; fi
+      KML_LIB=$L timeout -k 10 200 python bench.py $A --no-cpu-baseline --no-ber-match --full-loop-batches 0 > $O/${w}_${l}_$r.json 2> $O/${w}_${l}_$r.err || exit $?
+      python3 -c "import json,sys; d=json.loads(open('$O/${w}_${l}_$r.json').read().strip().splitlines()[-1]); print('$w $l $r', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['stats'].get('stage_ms_per_step'))" >> $O/summary.txt
+    done
+  done
+done
+cat $O/summary.txt
