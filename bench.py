@@ -378,7 +378,7 @@ def main():
     cw_err, _, c = ctx.sim_decode_ex(args.snr, blind=args.blind)
     e64 = cw_err.astype(np.float64)
     vals = np.array([c["err_bit"], c["err_blk"], c["tot_bit"], c["tot_blk"], c["vn_phases"], c["cn_phases"],
-                     e64.sum(), (e64 * e64).sum()], dtype=np.float64)
+                     e64.sum(), (e64 * e64).sum(), c.get("redone", 0)], dtype=np.float64)
 
     # full loop (untimed by the headline): GPU frame generation + decode, fresh frames per batch
     fl_n = max(0, args.full_loop_batches)
@@ -414,7 +414,7 @@ def main():
         return
     total_cw = B * args.steps * world
     value = total_cw / t_max
-    err_bit, err_blk, tot_bit, tot_blk, vn, cn, sum_e, sum_e2 = vals
+    err_bit, err_blk, tot_bit, tot_blk, vn, cn, sum_e, sum_e2, redone = vals
     Kbits = tot_bit / max(tot_blk, 1)
     bp_avg_ms = bp["ms"] / max(bp["launches"], 1)
     bp_bytes = bp["bytes"] / max(bp["launches"], 1)
@@ -422,32 +422,42 @@ def main():
     achieved_gbs = bp_bytes / (bp_avg_ms * 1e-3) / 1e9 if bp_avg_ms > 0 else 0.0
     achieved_tf = bp_flops / (bp_avg_ms * 1e-3) / 1e12 if bp_avg_ms > 0 else 0.0
 
-    # PMC summary of the same kernel/workload (profiles/pmc_bp.json, tools/pmc_summary.py)
-    traffic, issue_view, frac_exec, pmc_note = None, None, None, "no PMC summary for this kernel/workload"
+    # PMC map entry of the same workload and kernel family (profiles/pmc_bp.json, tools/kernel_evidence.py)
+    traffic, issue_view, frac_exec, pmc_note, pmc_others = None, None, None, "no PMC entry for this kernel/workload", None
     pmc = os.path.join(REPO, "profiles", "pmc_bp.json")
+    fam = bp_kernel.split()[0]
     if os.path.exists(pmc):
         try:
             pm = json.load(open(pmc))
-            if (pm.get("batch") == B and pm.get("workload") == args.matrix and not args.blind
-                    and pm.get("kernel") == bp_kernel.split()[0]):
-                current = pm.get("src_sha") == src_sha()
-                pmc_note = (f"profiles/pmc_bp.json ({pm.get('round', '?')}), "
+            ent = [e for e in pm.get("entries", []) if e.get("matrix") == args.matrix
+                   and bool(e.get("blind")) == bool(args.blind) and e.get("batch") == B and fam in e.get("kernels", {})]
+            if ent:
+                e = ent[-1]
+                k = e["kernels"][fam]
+                current = e.get("src_sha") == src_sha()
+                pmc_note = (f"profiles/pmc_bp.json entry {e.get('name')} ({e.get('round', '?')}), "
                             + ("taken at these kernel sources" if current else
-                               "STALE: taken at other kernel sources (src_sha differs)"))
-                traffic = pm.get("hbm_bytes_per_launch")
-                if pm.get("fp64_flops_executed_per_launch"):
-                    fe = pm["fp64_flops_executed_per_launch"]
+                               "STALE: taken at other kernel sources (src_sha differs)")
+                            + f"; rocprofv3 avg per launch chain {k.get('avg_ms')} ms")
+                traffic = k.get("hbm_bytes_per_launch")
+                if k.get("fp64_flops_executed_per_launch"):
+                    fe = k["fp64_flops_executed_per_launch"]
                     frac_exec = {"fp64_flops_executed_per_launch": fe,
                                  "achieved": round(fe / (bp_avg_ms * 1e-3) / 1e12, 2),
                                  "frac": round(fe / (bp_avg_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4),
                                  "rule": "64 x SQ_INSTS_VALU_FLOPS_FP64 per launch (PMC) / this run's avg launch time"}
-                if pm.get("valu_issue_busy_frac") is not None:
-                    issue_view = {"valu_issue_busy_frac": pm["valu_issue_busy_frac"],
-                                  "valu_wave_instr_per_launch": pm["valu_wave_instr_per_launch"],
+                if k.get("valu_issue_busy_frac") is not None:
+                    issue_view = {"valu_issue_busy_frac": k["valu_issue_busy_frac"],
+                                  "valu_wave_instr_per_launch": k.get("valu_wave_instr_per_launch"),
+                                  "lds_bank_conflict_frac": k.get("lds_bank_conflict_frac"),
                                   "rule": "SIMD cycles the VALU instruction stream occupies (4 per wave64 "
                                           "instruction, 16 per v_rcp_f64) / SIMD cycles of the launch"}
-        except Exception:
-            traffic = None
+                # the workload's other kernels (k-means, candidate metric, demap), same PMC runs
+                pmc_others = {n: {x: v[x] for x in ("avg_ms", "hbm_GBs", "hbm_frac", "fp64_TFLOPs", "fp64_frac",
+                                                    "lds_bank_conflict_frac") if x in v}
+                              for n, v in e["kernels"].items() if n != fam and v.get("avg_ms", 0) >= 0.05}
+        except Exception as ex:  # a malformed map is reported, never fatal
+            pmc_note = f"profiles/pmc_bp.json unreadable: {ex}"
 
     stats = {
         "fer": err_blk / max(tot_blk, 1),
@@ -456,6 +466,8 @@ def main():
         "codewords": int(tot_blk),
         "mean_cn_phases": cn / max(tot_blk, 1),
         "mean_vn_phases": vn / max(tot_blk, 1),
+        # codewords the FAST kernel could not prove correctly rounded and the EXACT kernel redid
+        "redone": int(redone),
         "stage_ms_per_step": {s: round(v["ms"] / max(args.steps, 1), 4) for s, v in stages.items() if v["launches"]},
         "bp_ms_per_step": round(bp["ms"] / max(args.steps, 1), 4),
     }
@@ -549,6 +561,7 @@ def main():
             "frac_executed": frac_exec,
             "issue_view": issue_view,
             "pmc": pmc_note,
+            "pmc_other_kernels": pmc_others,
             "hbm_view": {
                 "counter_bytes_per_launch": traffic,
                 "counter_GBs": round(traffic / (bp_avg_ms * 1e-3) / 1e9, 1) if traffic and bp_avg_ms > 0 else None,

@@ -33,7 +33,8 @@
  * Conventions
  *   - Every call returns 0 on success or a negative KML_E* code and never exits
  *     the process (the reference logs and exit(-1)s).  kml_last_error() holds
- *     the message of the last failure on that context.
+ *     the message of the last failure on that context (with a NULL context: the
+ *     last failure of a context-free call, kml_comm_unique_id, on this thread).
  *   - Bits (uu, uu_hat, cc_hat) are one byte per bit (0/1) unless a name says
  *     "_bits" (packed little-endian uint64 words).  Complex numbers are
  *     interleaved (re, im) doubles.

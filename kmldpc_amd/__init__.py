@@ -38,7 +38,7 @@ def comm_unique_id():
     u = np.zeros(128, np.uint8)
     r = lib().kml_comm_unique_id(_p(u))
     if r != 0:
-        raise KmlError(f"kml_comm_unique_id failed (code {r}): librccl.so.1 not loadable?")
+        raise KmlError(f"{lib().kml_last_error(None).decode()} (code {r})")
     return u.tobytes()
 
 

@@ -163,10 +163,10 @@ __device__ __forceinline__ void cn_norm_rows(const double (&n0)[R], const double
 //   FAST, VN: exact_div.hpp dd_quot — faithful always, and proven correctly
 //     rounded by dd_check; a quotient the check cannot prove sets sus, and the
 //     caller redoes the codeword on the exact path (FAST = false).  The FAST
-//     path runs only for codewords whose priors are 0, 1 or in
-//     [2^-40, 1-2^-40] on codes with column degree <= 20, which keeps every
-//     nonzero message, sum and quotient in [2^-840, 2] ("Exact
-//     division"), inside dd_check's domain.
+//     path runs only for codewords whose priors pass fast_prior_ok (on codes
+//     with column degree <= 23), which keeps every nonzero numerator at or
+//     above 2^-961 and every sum and quotient normal ("Division"),
+//     inside dd_check's domain.
 //   !FAST: div_rn (any operands).
 template <bool FAST, bool CN = false>
 __device__ __forceinline__ void div2(double n0, double n1, double s, double &q0, double &q1, bool &sus) {
@@ -209,14 +209,24 @@ __device__ __forceinline__ double div1(double n0, double s) {
 // (c0, RN(1 - c0)) directly; c2v messages are always clipped to
 // [1e-12, 1 - 1e-12] or 0.5 on the FAST path.
 
-// Prior values for which the FAST division path is exact (see div2).
+// Prior values for which the FAST division path is exact (see div2): +0, 1,
+// and q with q >= lo and 1 - q >= lo, lo = fast_prior_lo(dv_max) =
+// 2^(40 dv_max - 960).  Every quantity a FAST decode divides is a product of a
+// prior component and at most dv_max c2v components (each >= 1e-12 > 2^-40,
+// ProbClip), renormalised along the way (which only raises it), so it is 0 or
+// at least lo 2^(-40 dv_max) (1 - 2^-50) >= 2^-961 > 2^-969: inside the
+// residual-exactness domain of dd_check and of the near-one CN division.
 // -0.0 is excluded: with every prior >= +0 no message is ever -0, which makes
 // the x*1.0 / (1,0)-state identities used on the FAST path exact.
-__device__ __forceinline__ bool fast_prior_ok(double q) {
-  return (q == 0.0 && __double_as_longlong(q) == 0) || q == 1.0 || (q >= 0x1p-40 && q <= 1.0 - 0x1p-40);
+__device__ __forceinline__ double fast_prior_lo(int dv_max) {
+  return __longlong_as_double((long long)(63 + 40 * dv_max) << 52);  // 2^(40 dv_max - 960)
+}
+__device__ __forceinline__ bool fast_prior_ok(double q, double lo) {
+  return (q == 0.0 && __double_as_longlong(q) == 0) || q == 1.0 || (q >= lo && 1.0 - q >= lo);
 }
 
-constexpr int kFastMaxColumnDegree = 20;
+// lo = 2^-40 at dv_max = 23; beyond it no prior but 0 and 1 would qualify
+constexpr int kFastMaxColumnDegree = 23;
 
 // ProbClip of a c2v message (binaryldpccodec.cc:260-263).  On the FAST path the
 // value is finite (no NaN), where min(max(q, lo), hi) is the same two tests.

@@ -336,6 +336,7 @@ __device__ __forceinline__ int coop_iterations(const DevCode &c, const BpLaunch 
 template <int kG, int T, int RV, int RC, bool SYN, bool EXACT>
 __global__ __launch_bounds__(T) void bp_coop_kernel(DevCode c, BpLaunch a, GroupSync *gsync, uint8_t *gcch,
                                                     unsigned *abort, unsigned int *queue, int fast_allowed) {
+  const double plo = fast_prior_lo(c.dv_max);  // FAST prior domain (bp_common.hpp)
   const int tid = threadIdx.x;
   const int odd = tid & 1;
   const int member = (blockIdx.x >> 3) % kG;
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(T) void bp_coop_kernel(DevCode c, BpLaunch a, Group
 #pragma unroll
     for (int r = 0; r < RV; ++r) {
       pv[r] = (vcol[r] >= c.punct) ? p0[vcol[r] - c.punct] : 0.5;
-      ok = ok && fast_prior_ok(pv[r]);
+      ok = ok && fast_prior_ok(pv[r], plo);
     }
     // InitMsg on this member's share of the slots
     {
@@ -1270,6 +1271,7 @@ __device__ __forceinline__ int part_iterations_tagged(
 template <int kG, int T, int RV, int RC, int RX, bool SYN, bool TAGGED, bool EXACT>
 __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, GroupSync *gsync, uint8_t *gcch,
                                                     unsigned *abort, unsigned int *queue, int fast_allowed) {
+  const double plo = fast_prior_lo(c.dv_max);  // FAST prior domain (bp_common.hpp)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int DV = 3, DC = 6;
   const int tid = threadIdx.x;
@@ -1370,7 +1372,7 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     for (int r = 0; r < RV; ++r) {
       const int col = c.pt_vn[vpos[r]];
       pv[r] = (col >= c.punct) ? p0[col - c.punct] : 0.5;
-      ok = ok && fast_prior_ok(pv[r]);
+      ok = ok && fast_prior_ok(pv[r], plo);
     }
     // InitMsg: row slots and mirror slots (c2v = 0.5)
     for (int e = tid; e < nslots; e += T) reinterpret_cast<double2 *>(smem)[e] = make_double2(0.5, 0.5);

@@ -423,6 +423,7 @@ __device__ __forceinline__ bool decode_irr(const DevCode &c, const BpLaunch &a, 
 // EXACT = true: the exact path over the defer list (see bp_regular.hip).
 template <int T, bool SYN, bool EXACT>
 __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, unsigned int *queue, int fast_allowed) {
+  const double plo = fast_prior_lo(c.dv_max);  // FAST prior domain (bp_common.hpp)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) int pflags[16];  // wg_all of the FAST prior check (bp_common.hpp)
   const int tid = threadIdx.x;
@@ -461,7 +462,7 @@ __global__ __launch_bounds__(T) void bp_irregular_kernel(DevCode c, BpLaunch a, 
     for (int i = tid; i < c.cc_len; i += T) {
       const double q = p0[i];
       p0s[i] = q;
-      ok = ok && fast_prior_ok(q);
+      ok = ok && fast_prior_ok(q, plo);
     }
     for (int e = tid; e < c.irr_slots; e += T) slots[e].x = 0.5;  // InitMsg
     const bool fast = wg_all<T / 64>(ok ? 1 : 0, pflags) && (fast_allowed & 1);

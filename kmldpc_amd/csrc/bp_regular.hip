@@ -365,6 +365,7 @@ constexpr size_t reg_lds_bytes(int E, int N, int K, int DMB) { return ipos_offse
 // would otherwise be allocated (and spilled) in the FAST kernel too.
 template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB, bool EXACT>
 __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, unsigned int *queue, int fast_allowed) {
+  const double plo = fast_prior_lo(c.dv_max);  // FAST prior domain (bp_common.hpp)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) int pflags[16];  // wg_all of the FAST prior check (bp_common.hpp)
   // fused demap: the constellation and the exp table in LDS (demap_common.hpp)
@@ -438,7 +439,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
         const double2 v = yy[j];
         double out[DMB];
         if constexpr (EXACT)
-          demap_symbol<DMB>((lds_cons)dcons, (lds_exptab)detab, v.x, v.y, hh.x, hh.y, a.sym_var, out);
+          demap_symbol_t<DMB, false>((lds_cons)dcons, (lds_exptab)detab, v.x, v.y, hh.x, hh.y, a.sym_var, out);
         else  // no exact fallback in the FAST kernel (its registers): a failing symbol defers the codeword
           dok &= demap_symbol_t<DMB, true>((lds_cons)dcons, (lds_exptab)detab, v.x, v.y, hh.x, hh.y, a.sym_var, out);
 #pragma unroll
@@ -457,7 +458,7 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
 #pragma unroll
     for (int r = 0; r < RV; ++r) {
       pv[r] = (vcol[r] >= c.punct) ? p0[vcol[r] - c.punct] : 0.5;
-      ok = ok && fast_prior_ok(pv[r]);
+      ok = ok && fast_prior_ok(pv[r], plo);
     }
     const bool fast = wg_all<T / 64>(ok ? 1 : 0, pflags) && (fast_allowed & 1);
     REG_STAMP(2);

@@ -90,6 +90,7 @@ struct kml_ctx {
   kml::RcclComm *comm = nullptr;  // counter all-reduce over the ranks (kml_comm_init)
   DBuf w_comm;
   DBuf w_defer;  // BP launches: codewords the FAST kernel leaves to the exact kernel (+ count)
+  DBuf w_ddefer;  // demap / candidate-metric launches: the same for symbols or codewords
   // workspaces
   DBuf w_y, w_h, w_h4, w_hhat, w_p0, w_uu, w_uh, w_uh4, w_ret, w_cch, w_syn, w_sel, w_met, w_pc, w_cnt, w_km, w_cwerr;
   // soft syndrome metric: candidate / final syndromes, iteration counts, sums, decode lists
@@ -413,6 +414,17 @@ int run_bp(kml_ctx *c, kml::BpLaunch a, int &slot_out, int reuse = -1) {
   return KML_OK;
 }
 
+// The FAST demappers' defer list (kernels.hpp DemapDefer): at least `need`
+// entries (the candidate metric defers whole codewords: need = B).
+int demap_defer(kml_ctx *c, int need, kml::DemapDefer &d) {
+  const int cap = std::max(need, 65536);
+  HIPCHK(c, c->w_ddefer.ensure(sizeof(int32_t) * ((size_t)cap + 16)), "hipMalloc(demap defer list)");
+  d.idx = c->w_ddefer.as<int32_t>();
+  d.cnt = reinterpret_cast<unsigned *>(d.idx + cap);
+  d.cap = cap;
+  return KML_OK;
+}
+
 // Stage a host or device input; returns a device pointer.
 template <class T>
 int stage_in(kml_ctx *c, DBuf &buf, const T *src, size_t n, int flags, const T *&dev) {
@@ -528,8 +540,10 @@ int receive(kml_ctx *c, const RecvIO &io, double snr, int B, int &bp_slot) {
   if (io.true_h && !io.histogram) {  // known channel: one demap + BP
     HIPCHK(c, c->w_p0.ensure(sizeof(double) * cc * B), "hipMalloc(p0)");
     Timer t(c, "demap", -1, (double)B * S * (16.0 + 8.0 * c->modem.bits));
+    kml::DemapDefer dd;
+    TRY(demap_defer(c, 0, dd));
     HIPCHK(c, kml::launch_demap(c->modem.bits, cons, io.y, S, 1, io.true_h, 1, nullptr, var, B, c->w_p0.as<double>(),
-                                c->stream),
+                                dd, c->stream),
            "demap");
     t.stop();
     a.p0 = c->w_p0.as<double>();
@@ -582,7 +596,9 @@ int receive(kml_ctx *c, const RecvIO &io, double snr, int B, int &bp_slot) {
   }
   if (!c->code.is5g) {  // hard metric on the demapper output (kmcodec.cc:109-117)
     Timer t(c, "metric", -1, (double)B * nc * S * 16.0);
-    HIPCHK(c, kml::launch_cand_metric(c->dc, c->modem.bits, cons, io.y, S, hc, nc, var, B, met, chosen, c->stream),
+    kml::DemapDefer dd;
+    TRY(demap_defer(c, B, dd));
+    HIPCHK(c, kml::launch_cand_metric(c->dc, c->modem.bits, cons, io.y, S, hc, nc, var, B, met, chosen, dd, c->stream),
            "cand_metric");
     t.stop();
     if (io.histogram) {
@@ -605,7 +621,7 @@ int receive(kml_ctx *c, const RecvIO &io, double snr, int B, int &bp_slot) {
     HIPCHK(c, c->w_p0.ensure(sizeof(double) * cc * B), "hipMalloc(p0)");
     Timer t2(c, "demap", -1, (double)B * S * (16.0 + 8.0 * c->modem.bits));
     HIPCHK(c, kml::launch_demap(c->modem.bits, cons, io.y, S, 1, hc, nc, chosen, var, B, c->w_p0.as<double>(),
-                                c->stream),
+                                dd, c->stream),
            "demap");
     t2.stop();
     a.p0 = c->w_p0.as<double>();
@@ -617,8 +633,10 @@ int receive(kml_ctx *c, const RecvIO &io, double snr, int B, int &bp_slot) {
   HIPCHK(c, c->w_pc.ensure(sizeof(int32_t) * nc * B), "hipMalloc(pc)");
   {
     Timer t(c, "demap", -1, (double)nc * B * S * (16.0 + 8.0 * c->modem.bits));
+    kml::DemapDefer dd;
+    TRY(demap_defer(c, 0, dd));
     HIPCHK(c, kml::launch_demap(c->modem.bits, cons, io.y, S, nc, hc, 1, nullptr, var, nc * B, c->w_p0.as<double>(),
-                                c->stream),
+                                dd, c->stream),
            "demap candidates");
     t.stop();
   }
@@ -679,8 +697,10 @@ int soft_receive(kml_ctx *c, const RecvIO &io, double var, int B, const double2 
   HIPCHK(c, c->s_Lm.ensure(sizeof(double) * nB), "hipMalloc(L)");
   {
     Timer t(c, "demap", -1, (double)nB * S * (16.0 + 8.0 * c->modem.bits));
+    kml::DemapDefer dd;
+    TRY(demap_defer(c, 0, dd));
     HIPCHK(c, kml::launch_demap(c->modem.bits, cons, io.y, S, nc, hc, 1, nullptr, var, (int)nB, c->w_p0.as<double>(),
-                                c->stream),
+                                dd, c->stream),
            "demap candidates");
     t.stop();
   }
@@ -889,6 +909,7 @@ void kml_destroy(kml_ctx *c) {
     c->comm = nullptr;
     c->w_comm.release();
     c->w_defer.release();
+    c->w_ddefer.release();
     for (DBuf *b : {&c->d_graph, &c->d_cons, &c->d_arena, &c->d_queue, &c->d_gslots, &c->d_gsync, &c->d_gcch, &c->w_y, &c->w_h, &c->w_h4,
                     &c->w_hhat, &c->w_p0, &c->w_uu, &c->w_uh, &c->w_uh4, &c->w_cwerr, &c->w_ret, &c->w_cch, &c->w_syn, &c->w_sel, &c->w_met,
                     &c->w_pc, &c->w_cnt, &c->w_km, &c->s_synm, &c->s_synf, &c->s_itm, &c->s_itf, &c->s_Lm, &c->s_Lf, &c->s_list, &c->s_sel, &c->s_uu, &c->s_cc, &c->s_y, &c->s_h, &c->w_hc})
@@ -899,7 +920,9 @@ void kml_destroy(kml_ctx *c) {
   delete c;
 }
 
-const char *kml_last_error(const kml_ctx *c) { return c ? c->err.c_str() : "null context"; }
+// context-free calls (kml_comm_unique_id) report through this thread's message
+static thread_local std::string g_free_err = "null context";
+const char *kml_last_error(const kml_ctx *c) { return c ? c->err.c_str() : g_free_err.c_str(); }
 
 const char *kml_bp_kernel(const kml_ctx *c) { return c && c->bp_family ? c->bp_family : ""; }
 
@@ -1002,8 +1025,10 @@ int kml_demap(kml_ctx *c, const double *y, const double *h, double var, int B, d
   double *d_p0;
   TRY(stage_out_ptr(c, c->w_p0, p0, (size_t)B * c->code.cc_len, flags, d_p0));
   Timer t(c, "demap", -1, (double)B * S * (16.0 + 8.0 * c->modem.bits));
+  kml::DemapDefer dd;
+  TRY(demap_defer(c, 0, dd));
   HIPCHK(c, kml::launch_demap(c->modem.bits, c->d_cons.as<double>(), reinterpret_cast<const double2 *>(d_y), S, 1,
-                              reinterpret_cast<const double2 *>(d_h), 1, nullptr, var, B, d_p0, c->stream),
+                              reinterpret_cast<const double2 *>(d_h), 1, nullptr, var, B, d_p0, dd, c->stream),
          "demap");
   t.stop();
   TRY(copy_out(c, p0, d_p0, (size_t)B * c->code.cc_len, flags));
@@ -1230,7 +1255,9 @@ int decode_frames_chunked(kml_ctx *c, const double *y, const double *true_h, dou
 int kml_comm_unique_id(uint8_t *id) {
   std::string err;
   if (!id) return KML_E_ARG;
-  return kml::rccl_unique_id(id, err) == 0 ? KML_OK : KML_E_UNSUP;
+  if (kml::rccl_unique_id(id, err) == 0) return KML_OK;
+  g_free_err = "kml_comm_unique_id: " + err;
+  return KML_E_UNSUP;
 }
 
 int kml_comm_init(kml_ctx *c, const uint8_t *id, int world, int rank) {

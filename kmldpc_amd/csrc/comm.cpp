@@ -27,17 +27,53 @@ struct RcclApi {
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
-  std::string why;
+  std::string why, path;
 };
+
+// The directory of the HIP runtime this library's kernels run on (the first
+// libamdhip64.so.7 the process loaded: /opt/rocm's when the library is loaded
+// before torch, torch's bundled copy otherwise).
+std::string hip_runtime_path(const void *fn) {
+  Dl_info info{};
+  if (!dladdr(fn, &info) || !info.dli_fname) return "";
+  return info.dli_fname;
+}
+
+std::string dir_of(const std::string &p) {
+  const size_t k = p.rfind('/');
+  return k == std::string::npos ? std::string() : p.substr(0, k + 1);
+}
 
 RcclApi &api() {
   static RcclApi a;
   if (a.tried) return a;
   a.tried = true;
-  void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  // librccl must run on the SAME HIP runtime as the library's streams.  Two
+  // runtimes can be mapped into one process (the library's /opt/rocm copy and
+  // torch's bundled one), and both librccl copies have the soname
+  // librccl.so.1, so dlopen("librccl.so.1") hands back whichever is already
+  // loaded (torch's, bound to torch's runtime: "unhandled cuda error" on the
+  // library's stream).  Open the librccl next to our runtime by path, then
+  // check what its HIP symbols resolve to.
+  const std::string ours = hip_runtime_path(reinterpret_cast<const void *>(&hipStreamSynchronize));
+  const std::string dir = dir_of(ours);
+  void *h = nullptr;
+  for (const std::string &cand : {dir + "librccl.so.1", dir + "librccl.so", std::string("/opt/rocm/lib/librccl.so.1")}) {
+    if (cand.empty() || cand[0] != '/') continue;
+    h = dlopen(cand.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (!h) continue;
+    const void *theirs = dlsym(h, "hipStreamSynchronize");
+    if (theirs && hip_runtime_path(theirs) == ours) {
+      a.path = cand;
+      break;
+    }
+    a.why += cand + " is bound to HIP runtime " + (theirs ? hip_runtime_path(theirs) : std::string("?")) +
+             ", the library runs on " + ours + "; ";
+    dlclose(h);
+    h = nullptr;
+  }
   if (!h) {
-    a.why = std::string("cannot load librccl.so.1: ") + dlerror();
+    a.why = "no librccl bound to the library's HIP runtime (" + ours + "): " + a.why;
     return a;
   }
   a.get_unique_id = reinterpret_cast<decltype(a.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
@@ -46,7 +82,7 @@ RcclApi &api() {
   a.destroy = reinterpret_cast<decltype(a.destroy)>(dlsym(h, "ncclCommDestroy"));
   a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(h, "ncclGetErrorString"));
   a.ok = a.get_unique_id && a.init_rank && a.all_reduce && a.destroy && a.error_string;
-  if (!a.ok) a.why = "librccl.so.1 lacks an NCCL entry point";
+  if (!a.ok) a.why = a.path + " lacks an NCCL entry point";
   return a;
 }
 
@@ -92,7 +128,7 @@ RcclComm *rccl_init(const unsigned char *id, int world, int rank, std::string &e
   c->rank = rank;
   const ncclResult_t r = a.init_rank(&c->comm, world, uid, rank);  // collective over the world's ranks
   if (r != ncclSuccess) {
-    err = "ncclCommInitRank: " + nccl_err(r);
+    err = "ncclCommInitRank (" + a.path + "): " + nccl_err(r);
     delete c;
     return nullptr;
   }

@@ -27,54 +27,70 @@ namespace kml {
 
 namespace {
 
-template <int MB>
+// FAST (EXACT = false): every symbol on the proven FAST path; a symbol it
+// cannot prove gets the sentinel p0 = -1 in its first bit and its index on the
+// defer list (d.idx, up to d.cap entries; the count runs on past the cap).
+// EXACT: the listed symbols on the exact path (div_rn, kml_exp), or, when the
+// list overflowed, every symbol carrying the sentinel.
+template <int MB, bool EXACT>
 __global__ __launch_bounds__(256) void demap_kernel(const double *__restrict__ cons, const double2 *__restrict__ y,
                                                     int S, int reps, const double2 *__restrict__ h, int h_stride,
                                                     const int32_t *__restrict__ h_sel, double var, int B,
-                                                    double *__restrict__ p0) {
+                                                    double *__restrict__ p0, DemapDefer d) {
   __shared__ double cl[2 << MB];  // the constellation, read with uniform LDS loads
   __shared__ uint64_t etab[256];
+  const long long n = (long long)B * S;
+  long long todo = n;
+  bool listed = false;
+  if constexpr (EXACT) {
+    const unsigned cnt = *d.cnt;
+    if (cnt == 0) return;
+    listed = cnt <= (unsigned)d.cap;
+    if (listed) todo = cnt;
+  }
   for (int k = threadIdx.x; k < (2 << MB); k += blockDim.x) cl[k] = cons[k];
   stage_exp_table(etab);
   __syncthreads();
   // grid-stride over the symbols: the LDS staging above is paid once per
   // workgroup, not once per 256 symbols
-  const long long n = (long long)B * S;
-  for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < n;
-       gid += (long long)gridDim.x * blockDim.x) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < todo; i += (long long)gridDim.x * blockDim.x) {
+    const long long gid = listed ? (long long)(unsigned)d.idx[i] : i;
+    if (EXACT && !listed && !(p0[gid * MB] < 0.0)) continue;
     const int ent = (int)(gid / S);
     const int j = (int)(gid - (long long)ent * S);
     const double2 hh = h[(long long)ent * h_stride + (h_sel ? h_sel[ent] : 0)];
     const double2 yy = y[(long long)(ent / reps) * S + j];
     double out[MB];
-    demap_symbol<MB>((lds_cons)cl, (lds_exptab)etab, yy.x, yy.y, hh.x, hh.y, var, out);
+    if constexpr (EXACT) {
+      demap_symbol_t<MB, false>((lds_cons)cl, (lds_exptab)etab, yy.x, yy.y, hh.x, hh.y, var, out);
+    } else if (!demap_symbol_t<MB, true>((lds_cons)cl, (lds_exptab)etab, yy.x, yy.y, hh.x, hh.y, var, out)) {
+      p0[gid * MB] = -1.0;  // the sentinel (a P0 is in [1e-12, 1 - 1e-12])
+      const unsigned k = atomicAdd(d.cnt, 1u);
+      if (k < (unsigned)d.cap) d.idx[k] = (int32_t)gid;
+      continue;
+    }
 #pragma unroll
     for (int b = 0; b < MB; ++b) p0[gid * MB + b] = out[b];
   }
 }
 
-// One workgroup per codeword: hard decisions of the candidates into LDS, then
-// the unsatisfied-check counts.  The (candidate, symbol) pairs are flattened
-// over the workgroup; each symbol's decisions come from the single-precision
-// screen (hard_bits_screen) unless a bit is too close to call, in which case
-// the exact demapper decides.
-template <int MB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? 3 : 1))) void cand_metric_kernel(DevCode c, const double *__restrict__ cons,
-                                                          const double2 *__restrict__ y, int S,
-                                                          const double2 *__restrict__ h4, int nc, double var,
-                                                          double inv_var, double *__restrict__ metrics,
-                                                          int32_t *__restrict__ chosen) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int *cnt = reinterpret_cast<int *>(smem);  // 4 counters + the undecided flag
+// One codeword: hard decisions of its candidates into LDS, then the
+// unsatisfied-check counts.  The (candidate, symbol) pairs are flattened over
+// the workgroup; each symbol's decisions come from the single-precision screen
+// (hard_bits_screen) unless a bit is too close to call, in which case the
+// demapper decides: the FAST one (EXACT = false), which leaves the codeword to
+// the EXACT kernel when it cannot prove a symbol (returns false, nothing
+// written), or the exact one.
+template <int MB, bool EXACT>
+__device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const double2 *__restrict__ y, int S,
+                                               const double2 *__restrict__ h4, int nc, double var, double inv_var,
+                                               double *__restrict__ metrics, int32_t *__restrict__ chosen,
+                                               unsigned char *smem, lds_cons cl, lds_exptab etab) {
+  int *cnt = reinterpret_cast<int *>(smem);  // 4 counters, the undecided flag, the unproven flag
   unsigned char *hb = smem + 32;             // [4][cc_len]
   constexpr bool kRescan = MB >= 5;
-  const int cw = blockIdx.x;
   const int tid = threadIdx.x;
-  __shared__ double cl[2 << MB];
-  __shared__ uint64_t etab[256];
-  for (int k = tid; k < (2 << MB); k += blockDim.x) cl[k] = cons[k];
-  stage_exp_table(etab);
-  if (tid < 5) cnt[tid] = 0;
+  if (tid < 6) cnt[tid] = 0;
   __syncthreads();
   const double2 *yy = y + (long long)cw * S;
   for (int i = tid; i < nc * S; i += blockDim.x) {
@@ -82,14 +98,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? 3
     const double2 v = yy[j];
     const double2 hh = h4[(long long)cw * nc + q];
     unsigned bits;
-    if (!hard_bits_screen<MB>((lds_cons)cl, v.x, v.y, hh.x, hh.y, inv_var, bits)) {
+    if (!hard_bits_screen<MB>(cl, v.x, v.y, hh.x, hh.y, inv_var, bits)) {
       if (kRescan) {
-        hb[q * c.cc_len + j * MB] = 2;  // undecided: the exact pass below
+        hb[q * c.cc_len + j * MB] = 2;  // undecided: the demap pass below
         cnt[4] = 1;
         continue;
       }
       double out[MB];
-      demap_symbol<MB>((lds_cons)cl, (lds_exptab)etab, v.x, v.y, hh.x, hh.y, var, out);
+      if constexpr (EXACT) {
+        demap_symbol_t<MB, false>(cl, etab, v.x, v.y, hh.x, hh.y, var, out);
+      } else if (!demap_symbol_t<MB, true>(cl, etab, v.x, v.y, hh.x, hh.y, var, out)) {
+        cnt[5] = 1;
+        continue;
+      }
       bits = 0;
 #pragma unroll
       for (int b = 0; b < MB; ++b) bits |= (out[b] > 0.5 ? 1u : 0u) << b;  // kmcodec.cc:111-115
@@ -98,20 +119,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? 3
     for (int b = 0; b < MB; ++b) hb[q * c.cc_len + j * MB + b] = (bits >> b) & 1;
   }
   __syncthreads();
-  if (kRescan && cnt[4]) {  // 64QAM: the exact demapper in a pass of its own
-                            // keeps its registers out of the screening loop's
+  if (kRescan && cnt[4]) {  // 64QAM: the demapper in a pass of its own keeps its
+                            // registers out of the screening loop's
     for (int i = tid; i < nc * S; i += blockDim.x) {
       const int q = i / S, j = i - q * S;
       if (hb[q * c.cc_len + j * MB] != 2) continue;
       const double2 v = yy[j];
       const double2 hh = h4[(long long)cw * nc + q];
       double out[MB];
-      demap_symbol<MB>((lds_cons)cl, (lds_exptab)etab, v.x, v.y, hh.x, hh.y, var, out);
+      if constexpr (EXACT) {
+        demap_symbol_t<MB, false>(cl, etab, v.x, v.y, hh.x, hh.y, var, out);
+      } else if (!demap_symbol_t<MB, true>(cl, etab, v.x, v.y, hh.x, hh.y, var, out)) {
+        cnt[5] = 1;
+        continue;
+      }
 #pragma unroll
       for (int b = 0; b < MB; ++b) hb[q * c.cc_len + j * MB + b] = out[b] > 0.5 ? 1 : 0;  // kmcodec.cc:111-115
     }
   }
   __syncthreads();
+  if (!EXACT && cnt[5]) return false;  // uniform: every thread read the flag after the barrier
   int local[4] = {0, 0, 0, 0};
   for (int r = tid; r < c.M; r += blockDim.x) {
     int p[4] = {0, 0, 0, 0};
@@ -135,6 +162,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? 3
       if (q < nc && cnt[q] < cnt[best]) best = q;
     }
     chosen[cw] = best;
+  }
+  __syncthreads();  // cnt and hb are reused by the next codeword
+  return true;
+}
+
+// FAST: one workgroup per codeword, unproven codewords onto the defer list
+// (at most B entries: d.cap >= B).  EXACT: the listed codewords, grid-stride.
+template <int MB, bool EXACT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? 3 : 1))) void cand_metric_kernel(
+    DevCode c, const double *__restrict__ cons, const double2 *__restrict__ y, int S, const double2 *__restrict__ h4,
+    int nc, double var, double inv_var, double *__restrict__ metrics, int32_t *__restrict__ chosen, DemapDefer d) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ double cl[2 << MB];
+  __shared__ uint64_t etab[256];
+  unsigned todo = 1;
+  if constexpr (EXACT) {
+    todo = *d.cnt;
+    if (blockIdx.x >= todo) return;
+  }
+  for (int k = threadIdx.x; k < (2 << MB); k += blockDim.x) cl[k] = cons[k];
+  stage_exp_table(etab);
+  __syncthreads();
+  if constexpr (EXACT) {
+    for (unsigned i = blockIdx.x; i < todo; i += gridDim.x)
+      cand_metric_cw<MB, true>(d.idx[i], c, y, S, h4, nc, var, inv_var, metrics, chosen, smem, (lds_cons)cl,
+                               (lds_exptab)etab);
+  } else {
+    const int cw = blockIdx.x;
+    if (!cand_metric_cw<MB, false>(cw, c, y, S, h4, nc, var, inv_var, metrics, chosen, smem, (lds_cons)cl,
+                                   (lds_exptab)etab) &&
+        threadIdx.x == 0)
+      d.idx[atomicAdd(d.cnt, 1u)] = cw;
   }
 }
 
@@ -232,43 +291,68 @@ hipError_t launch_soft_sum(const double *syn, int M, const int32_t *iters, const
 }
 
 hipError_t launch_demap(int bits, const double *cons, const double2 *y, int S, int reps, const double2 *h,
-                        int h_stride, const int32_t *h_sel, double var, int B, double *p0, hipStream_t s) {
+                        int h_stride, const int32_t *h_sel, double var, int B, double *p0, const DemapDefer &d,
+                        hipStream_t s) {
   const long long n = (long long)B * S;
   if (n == 0) return hipSuccess;
+  if (n > 0x7FFFFFFFLL || !d.idx || !d.cnt || d.cap < 1) return hipErrorInvalidValue;  // int32 symbol indices
   int dev = 0, ncu = 0;
   hipGetDevice(&dev);
   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  // small constellations: 8 workgroups per CU, grid-stride; 64QAM (three
-  // waves per SIMD, long symbols): one symbol per thread
+  // small constellations: 8 workgroups per CU, grid-stride; 64QAM (long
+  // symbols): one symbol per thread
   const long long wg = (n + 255) / 256;
   const dim3 grid((unsigned)(bits >= 5 ? wg : std::min<long long>(wg, 8LL * ncu))), blk(256);
+  const dim3 xgrid((unsigned)std::min<long long>(wg, 2LL * ncu));  // the exact pass: few symbols, or a scan
+  hipError_t e = hipMemsetAsync(d.cnt, 0, sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
   switch (bits) {
-    case 1: hipLaunchKernelGGL(demap_kernel<1>, grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0); break;
-    case 2: hipLaunchKernelGGL(demap_kernel<2>, grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0); break;
-    case 3: hipLaunchKernelGGL(demap_kernel<3>, grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0); break;
-    case 4: hipLaunchKernelGGL(demap_kernel<4>, grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0); break;
-    case 6: hipLaunchKernelGGL(demap_kernel<6>, grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0); break;
-    default: return hipErrorInvalidValue;
+#define KML_DM(MBV)                                                                                              \
+  case MBV:                                                                                                      \
+    hipLaunchKernelGGL((demap_kernel<MBV, false>), grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, \
+                       p0, d);                                                                                   \
+    hipLaunchKernelGGL((demap_kernel<MBV, true>), xgrid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, \
+                       p0, d);                                                                                   \
+    break;
+    KML_DM(1)
+    KML_DM(2)
+    KML_DM(3)
+    KML_DM(4)
+    KML_DM(6)
+#undef KML_DM
+    default:
+      return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
 hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, const double2 *y, int S,
                               const double2 *h4, int nc, double var, int B, double *metrics, int32_t *chosen,
-                              hipStream_t s) {
+                              const DemapDefer &d, hipStream_t s) {
   if (B == 0) return hipSuccess;
   if (nc < 1 || nc > 4) return hipErrorInvalidValue;
+  if (!d.idx || !d.cnt || d.cap < B) return hipErrorInvalidValue;  // every codeword may defer
   const size_t lds = 32 + 4 * (size_t)c.cc_len;
-  const dim3 grid(B), blk(256);
+  int dev = 0, ncu = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const dim3 grid(B), xgrid((unsigned)std::min(B, 2 * ncu)), blk(256);
+  hipError_t e = hipMemsetAsync(d.cnt, 0, sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
   switch (bits) {
-#define KML_CM(MBV)                                                                                          \
-  case MBV: {                                                                                                \
-    hipError_t e = hipFuncSetAttribute((const void *)cand_metric_kernel<MBV>,                                \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
-    if (e != hipSuccess) return e;                                                                           \
-    hipLaunchKernelGGL(cand_metric_kernel<MBV>, grid, blk, lds, s, c, cons, y, S, h4, nc, var, 1.0 / var, metrics, \
-                       chosen);                                                                              \
-    break;                                                                                                   \
+#define KML_CM(MBV)                                                                                             \
+  case MBV: {                                                                                                   \
+    e = hipFuncSetAttribute((const void *)cand_metric_kernel<MBV, false>,                                       \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                              \
+    if (e == hipSuccess)                                                                                        \
+      e = hipFuncSetAttribute((const void *)cand_metric_kernel<MBV, true>,                                      \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                            \
+    if (e != hipSuccess) return e;                                                                              \
+    hipLaunchKernelGGL((cand_metric_kernel<MBV, false>), grid, blk, lds, s, c, cons, y, S, h4, nc, var, 1.0 / var, \
+                       metrics, chosen, d);                                                                     \
+    hipLaunchKernelGGL((cand_metric_kernel<MBV, true>), xgrid, blk, lds, s, c, cons, y, S, h4, nc, var, 1.0 / var, \
+                       metrics, chosen, d);                                                                     \
+    break;                                                                                                      \
   }
     KML_CM(1)
     KML_CM(2)

@@ -83,6 +83,9 @@ template <int MB, bool FAST, class CP>
 __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double yr, double yi, double hr,
                                                double hi, double var, double *out) {
   constexpr int KC = 1 << MB;
+  // opaque per call: the constellation's LDS loads must not be hoisted out of
+  // the caller's symbol loop (64QAM: 128 doubles held live across it)
+  asm volatile("" : "+v"(cons), "+v"(etab));
   double pr[KC];
   double mx = 0.0;
   double nmin = 0.0, nmax = 0.0;
@@ -171,18 +174,11 @@ __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double 
   return dok;
 }
 
-template <int MB, class CP>
-__device__ __forceinline__ void demap_symbol(CP cons, lds_exptab etab, double yr, double yi, double hr, double hi,
-                                             double var, double *out) {
-  // 64QAM: the fast path's live state exceeds the 168 registers of three
-  // waves per SIMD (the compiler then runs one wave); the IEEE path fits
-  if (MB >= 5 || !demap_symbol_t<MB, true>(cons, etab, yr, yi, hr, hi, var, out)) {
-    // rare: reload the constellation rather than keep the fast path's loads
-    // live across it (they would pin 4 * KC registers)
-    asm volatile("" : "+v"(cons));
-    demap_symbol_t<MB, false>(cons, etab, yr, yi, hr, hi, var, out);
-  }
-}
+// Every kernel that demaps runs demap_symbol_t<MB, true> (FAST, proven) in a
+// FAST kernel and hands the symbols (or codewords) it cannot prove to an EXACT
+// kernel that runs demap_symbol_t<MB, false>: inlined side by side, the exact
+// path (div_rn, kml_exp) doubled the FAST kernels' registers and code, the
+// 64QAM demapper's past 300 KB (instruction-cache bound).
 
 // Hard decisions rr_j = (P0_j > 0.5) of one symbol's MB bits (the metric's
 // kmcodec.cc:111-115) screened in single precision: returns false when some bit

@@ -143,26 +143,33 @@ __device__ __forceinline__ double div_soft(double n, double s) {
   return __longlong_as_double((long long)(sign | out));
 }
 
+// RN(n / s) outside div_rn's fast domain: zeros, infinities and NaNs (IEEE
+// cases: hipcc's '/'), else the integer long division.  Out of line: it is
+// rare, and inlined at every division site it multiplied the exact kernels'
+// code size past the instruction cache.
+__device__ __noinline__ double div_rn_cold(double n, double s) {
+  const double an = fabs(n), as = fabs(s);
+  if (!(an > 0.0) || !(as > 0.0) || an == INFINITY || as == INFINITY) return n / s;  // 0, inf, NaN: IEEE cases
+  return div_soft(n, s);
+}
+
 // RN(n / s) for any operands (see 2. above).
 __device__ __forceinline__ double div_rn(double n, double s) {
   const double an = fabs(n), as = fabs(s);
-  if (an >= 0x1p-969 && an < 0x1p1000 && as >= 0x1p-1000 && as < 0x1p1000) {
+  if (__builtin_expect((an >= 0x1p-969) & (an < 0x1p1000) & (as >= 0x1p-1000) & (as < 0x1p1000), 1)) {
     const DdRcp y = dd_rcp(s);
     double q = dd_quot(n, y);
     const double aq = fabs(q);
-    if (aq >= 0x1p-1020 && aq < 0x1p1020) {
+    if (__builtin_expect((aq >= 0x1p-1020) & (aq < 0x1p1020), 1)) {
+      // the neighbour of q towards n / s (whose sign is r's times s's): an
+      // exact residual of 0 keeps q (|fma(-qn, s, n)| > 0)
       const double r = fma(-q, s, n);
-      if (r != 0.0) {
-        // the neighbour of q towards n / s (whose sign is r's times s's)
-        const long long step = ((r > 0.0) == (s > 0.0)) == (q > 0.0) ? 1 : -1;
-        const double qn = __longlong_as_double(__double_as_longlong(q) + step);
-        if (fabs(fma(-qn, s, n)) < fabs(r)) q = qn;
-      }
-      return q;
+      const long long step = ((r > 0.0) == (s > 0.0)) == (q > 0.0) ? 1 : -1;
+      const double qn = __longlong_as_double(__double_as_longlong(q) + step);
+      return fabs(fma(-qn, s, n)) < fabs(r) ? qn : q;
     }
   }
-  if (!(an > 0.0) || !(as > 0.0) || an == INFINITY || as == INFINITY) return n / s;  // 0, inf, NaN: IEEE cases
-  return div_soft(n, s);
+  return div_rn_cold(n, s);
 }
 
 }  // namespace kml

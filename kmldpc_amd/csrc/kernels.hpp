@@ -134,11 +134,20 @@ hipError_t launch_bp(const DevCode &c, const BpLaunch &a, hipStream_t s, const c
 long long bp_gslots_needed(const DevCode &c);
 bool bp_uses_lds(const DevCode &c);
 
+// The FAST demappers' defer list (demap.hip): symbol indices (launch_demap,
+// any cap; past it the exact pass scans for the sentinel) or codewords
+// (launch_cand_metric, cap >= B), and their device-side count.
+struct DemapDefer {
+  int32_t *idx = nullptr;
+  unsigned *cnt = nullptr;
+  int cap = 0;
+};
 // SoftAWGNDemodulation + Modem::DeMapping with bitLin = 0.5, for `n` entries:
 // entry e reads y row e / reps and channel h[e * h_stride + (h_sel ? h_sel[e] : 0)],
 // writes p0 row e.  (reps = 4, h_stride = 1 demaps the 4 blind candidates.)
 hipError_t launch_demap(int bits, const double *cons, const double2 *y, int S, int reps, const double2 *h,
-                        int h_stride, const int32_t *h_sel, double var, int n, double *p0, hipStream_t s);
+                        int h_stride, const int32_t *h_sel, double var, int n, double *p0, const DemapDefer &d,
+                        hipStream_t s);
 
 // Hard-metric candidates for the PEG blind path (kmcodec.cc:105-119):
 // for each codeword and each of its nc (1 or 4) channel estimates h4[b][j], the
@@ -146,7 +155,7 @@ hipError_t launch_demap(int bits, const double *cons, const double2 *y, int S, i
 // (entries >= nc zeroed), chosen[b] = first argmin.
 hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, const double2 *y, int S,
                               const double2 *h4, int nc, double var, int B, double *metrics, int32_t *chosen,
-                              hipStream_t s);
+                              const DemapDefer &d, hipStream_t s);
 // argmin over a [B][nc] parity-count table (first minimum) for the BP-based
 // metrics; metrics[b][4] = |count|.
 hipError_t launch_select(const int32_t *parity_cnt, int nc, int B, double *metrics, int32_t *chosen, hipStream_t s);
