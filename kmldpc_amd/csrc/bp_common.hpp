@@ -181,7 +181,7 @@ __device__ __forceinline__ void div2(double n0, double n1, double s, double &q0,
     const DdRcp y = dd_rcp(s);
     q0 = dd_quot(n0, y);
     q1 = dd_quot(n1, y);
-    sus |= !((int)dd_check(n0, s, q0, y) & (int)dd_check(n1, s, q1, y));
+    sus |= !((int)y.ok & (int)dd_check(n0, s, q0, y) & (int)dd_check(n1, s, q1, y));
   }
 }
 // the CN phase's form (near-one sums: nothing to prove at run time)

@@ -170,41 +170,33 @@ __device__ __forceinline__ int coop_iterations(const DevCode &c, const BpLaunch 
       for (int r = 0; r < RV; ++r)
 #pragma unroll
         for (int k = 0; k < DV; ++k) c0s[r][k] = ld_nt(&slots[es[r][k]].x);
-      double a0[RV], a1[RV], al0[RV][DV], al1[RV][DV];
+      // one column's chains at a time (column-major): the FAST divisions'
+      // proofs keep a normalisation's operands live, and interleaving the RV
+      // columns step by step doubled the live set (scratch spills in the loop)
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
-        a0[r] = pv[r];
-        a1[r] = 1.0 - pv[r];
-      }
+        double a0 = pv[r], a1 = 1.0 - pv[r], al0[DV], al1[DV];
 #pragma unroll
-      for (int k = 0; k < DV; ++k)
-#pragma unroll
-        for (int r = 0; r < RV; ++r) {
-          al0[r][k] = a0[r];
-          al1[r][k] = a1[r];
+        for (int k = 0; k < DV; ++k) {
+          al0[k] = a0;
+          al1[k] = a1;
           const double c0 = c0s[r][k];
-          const double n0 = a0[r] * c0;
-          const double n1 = a1[r] * (1.0 - c0);
+          const double n0 = a0 * c0;
+          const double n1 = a1 * (1.0 - c0);
           if (k + 1 < DV) {
-            div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r], sus);
+            div2<FAST>(n0, n1, n0 + n1, a0, a1, sus);
           } else {
             const int hd = hard_decision<FAST>(n0, n1, sus);
             if (vact[r]) gc[vpos[r]] = (unsigned char)hd;
           }
         }
-      double b0[RV], b1[RV];
+        if (r == RV / 2) __builtin_amdgcn_s_setprio(1);  // falling priorities within the phase
+        double b0 = 1.0, b1 = 1.0;
 #pragma unroll
-      for (int r = 0; r < RV; ++r) b0[r] = b1[r] = 1.0;
-      __builtin_amdgcn_s_setprio(2);
-#pragma unroll
-      for (int k = DV - 1; k >= 0; --k) {
-        if (k == DV - 2) __builtin_amdgcn_s_setprio(1);
-        if (k == DV - 3) __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-        for (int r = 0; r < RV; ++r) {
+        for (int k = DV - 1; k >= 0; --k) {
           const bool unit = FAST && k == DV - 1;
-          const double t0 = unit ? al0[r][k] : al0[r][k] * b0[r];
-          const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
+          const double t0 = unit ? al0[k] : al0[k] * b0;
+          const double t1 = unit ? al1[k] : al1[k] * b1;
           double q0, q1;
           if (unit)  // beta = (1, 1): t is the normalised alpha, its sum within ulps of 1 (bp_common.hpp rcp_near1)
             div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
@@ -214,14 +206,15 @@ __device__ __forceinline__ int coop_iterations(const DevCode &c, const BpLaunch 
           if (k > 0) {
             const double c0 = c0s[r][k];
             if (unit) {  // (c0, 1 - c0) / (c0 + (1 - c0)): the sum rounds to exactly 1 (bp_common.hpp)
-              b0[r] = c0;
-              b1[r] = 1.0 - c0;
+              b0 = c0;
+              b1 = 1.0 - c0;
             } else {
-              div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r], sus);
+              div2<FAST>(b0 * c0, b1 * (1.0 - c0), b0 * c0 + b1 * (1.0 - c0), b0, b1, sus);
             }
           }
         }
       }
+      __builtin_amdgcn_s_setprio(0);
     }
     if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return -1;
 
@@ -641,23 +634,21 @@ __device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, 
       for (int r = 0; r < RV; ++r)
 #pragma unroll
         for (int k = 0; k < DV; ++k) c0s[r][k] = *reinterpret_cast<const double *>(smem + (vaddr[r][k] & 0xFFFF) * 16);
-      double a0[RV], a1[RV], al0[RV][DV], al1[RV][DV];
+      // one column's chains at a time (column-major): the FAST divisions'
+      // proofs keep a normalisation's operands live, and interleaving the RV
+      // columns step by step doubled the live set (scratch spills in the loop)
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
-        a0[r] = pv[r];
-        a1[r] = 1.0 - pv[r];
-      }
+        double a0 = pv[r], a1 = 1.0 - pv[r], al0[DV], al1[DV];
 #pragma unroll
-      for (int k = 0; k < DV; ++k)
-#pragma unroll
-        for (int r = 0; r < RV; ++r) {
-          al0[r][k] = a0[r];
-          al1[r][k] = a1[r];
+        for (int k = 0; k < DV; ++k) {
+          al0[k] = a0;
+          al1[k] = a1;
           const double c0 = c0s[r][k];
-          const double n0 = a0[r] * c0;
-          const double n1 = a1[r] * (1.0 - c0);
+          const double n0 = a0 * c0;
+          const double n1 = a1 * (1.0 - c0);
           if (k + 1 < DV) {
-            div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r], sus);
+            div2<FAST>(n0, n1, n0 + n1, a0, a1, sus);
           } else {
             const int hd = hard_decision<FAST>(n0, n1, sus);
             if (vact[r]) {
@@ -666,19 +657,13 @@ __device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, 
             }
           }
         }
-      double b0[RV], b1[RV];
+        if (r == RV / 2) __builtin_amdgcn_s_setprio(1);  // falling priorities within the phase
+        double b0 = 1.0, b1 = 1.0;
 #pragma unroll
-      for (int r = 0; r < RV; ++r) b0[r] = b1[r] = 1.0;
-      __builtin_amdgcn_s_setprio(2);
-#pragma unroll
-      for (int k = DV - 1; k >= 0; --k) {
-        if (k == DV - 2) __builtin_amdgcn_s_setprio(1);
-        if (k == DV - 3) __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-        for (int r = 0; r < RV; ++r) {
+        for (int k = DV - 1; k >= 0; --k) {
           const bool unit = FAST && k == DV - 1;
-          const double t0 = unit ? al0[r][k] : al0[r][k] * b0[r];
-          const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
+          const double t0 = unit ? al0[k] : al0[k] * b0;
+          const double t1 = unit ? al1[k] : al1[k] * b1;
           double q0, q1;
           if (unit)  // beta = (1, 1): t is the normalised alpha, its sum within ulps of 1 (bp_common.hpp rcp_near1)
             div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
@@ -688,14 +673,15 @@ __device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, 
           if (k > 0) {
             const double c0 = c0s[r][k];
             if (unit) {  // the sum rounds to exactly 1 (bp_common.hpp)
-              b0[r] = c0;
-              b1[r] = 1.0 - c0;
+              b0 = c0;
+              b1 = 1.0 - c0;
             } else {
-              div2<FAST>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r], sus);
+              div2<FAST>(b0 * c0, b1 * (1.0 - c0), b0 * c0 + b1 * (1.0 - c0), b0, b1, sus);
             }
           }
         }
       }
+      __builtin_amdgcn_s_setprio(0);
     }
     KML_STAMP(2);  // VN compute (wave 0)
     // ---------------------------------------------- send v2c of the cut edges
@@ -1016,47 +1002,35 @@ __device__ __forceinline__ int part_iterations_tagged(
 #pragma unroll
         for (int k = 0; k < DV; ++k)
           c0s[r][k] = *reinterpret_cast<const double *>(smem + (vaddr[r][k] & 0xFFFF) * 16);
-      double a0[RV], a1[RV], al0[RV][DV], al1[RV][DV];
-      unsigned hdb[RV];
+      // one column's chains at a time (column-major): the FAST divisions'
+      // proofs keep a normalisation's operands live, and interleaving the RV
+      // columns step by step doubled the live set (scratch spills in the loop)
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
-        a0[r] = pv[r];
-        a1[r] = 1.0 - pv[r];
-      }
+        double a0 = pv[r], a1 = 1.0 - pv[r], al0[DV], al1[DV];
+        unsigned hdb = 0;
 #pragma unroll
-      for (int k = 0; k < DV; ++k)
-#pragma unroll
-        for (int r = 0; r < RV; ++r) {
-          al0[r][k] = a0[r];
-          al1[r][k] = a1[r];
+        for (int k = 0; k < DV; ++k) {
+          al0[k] = a0;
+          al1[k] = a1;
           const double c0 = c0s[r][k];
-          const double n0 = a0[r] * c0;
-          const double n1 = a1[r] * (1.0 - c0);
+          const double n0 = a0 * c0;
+          const double n1 = a1 * (1.0 - c0);
           if (k + 1 < DV) {
-            div2<true>(n0, n1, n0 + n1, a0[r], a1[r], sus);
+            div2<true>(n0, n1, n0 + n1, a0, a1, sus);
           } else {
             const int hd = hard_decision<true>(n0, n1, sus);
-            hdb[r] = hd ? kHdHi : 0u;
+            hdb = hd ? kHdHi : 0u;
             if (vact[r]) decb[r * T + tid] = (unsigned char)hd;
           }
         }
-      double b0[RV], b1[RV];
+        if (r == RV / 2) __builtin_amdgcn_s_setprio(1);  // falling priorities within the phase
+        double b0 = 1.0, b1 = 1.0;
 #pragma unroll
-      for (int r = 0; r < RV; ++r) b0[r] = b1[r] = 1.0;
-#if !KML_PART_VN_AGE_PRIO
-      __builtin_amdgcn_s_setprio(2);
-#endif
-#pragma unroll
-      for (int k = DV - 1; k >= 0; --k) {
-#if !KML_PART_VN_AGE_PRIO
-        if (k == DV - 2) __builtin_amdgcn_s_setprio(1);
-        if (k == DV - 3) __builtin_amdgcn_s_setprio(0);
-#endif
-#pragma unroll
-        for (int r = 0; r < RV; ++r) {
+        for (int k = DV - 1; k >= 0; --k) {
           const bool unit = k == DV - 1;
-          const double t0 = unit ? al0[r][k] : al0[r][k] * b0[r];
-          const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
+          const double t0 = unit ? al0[k] : al0[k] * b0;
+          const double t1 = unit ? al1[k] : al1[k] * b1;
           double q0, q1;
           if (unit)
             div2<true, true>(t0, t1, t0 + t1, q0, q1, sus);
@@ -1066,22 +1040,23 @@ __device__ __forceinline__ int part_iterations_tagged(
             const int x1 = vaddr[r][k] >> 16;  // mailbox index + 1 of a cut edge, 0 for a row slot
             if (x1) {
               const unsigned tb_tag = tag ? kTagHi : 0u;
-              mb_st128(tb, (unsigned)(x1 - 1) * 16, or_hi(q0, tb_tag | hdb[r]), or_hi(q1, tb_tag));
+              mb_st128(tb, (unsigned)(x1 - 1) * 16, or_hi(q0, tb_tag | hdb), or_hi(q1, tb_tag));
             } else {
-              *reinterpret_cast<double2 *>(smem + (vaddr[r][k] & 0xFFFF) * 16) = make_double2(or_hi(q0, hdb[r]), q1);
+              *reinterpret_cast<double2 *>(smem + (vaddr[r][k] & 0xFFFF) * 16) = make_double2(or_hi(q0, hdb), q1);
             }
           }
           if (k > 0) {
             const double c0 = c0s[r][k];
             if (unit) {
-              b0[r] = c0;
-              b1[r] = 1.0 - c0;
+              b0 = c0;
+              b1 = 1.0 - c0;
             } else {
-              div2<true>(b0[r] * c0, b1[r] * (1.0 - c0), b0[r] * c0 + b1[r] * (1.0 - c0), b0[r], b1[r], sus);
+              div2<true>(b0 * c0, b1 * (1.0 - c0), b0 * c0 + b1 * (1.0 - c0), b0, b1, sus);
             }
           }
         }
       }
+      __builtin_amdgcn_s_setprio(0);
     }
     KML_STAMP(2);
     // ------------------- receive v2c of the cut edges; the previous CN's flags

@@ -10,29 +10,30 @@
 // provably RN(n / s).
 //
 // 1. dd_quot + dd_check (the decoders' FAST VN divisions, demap_common.hpp):
-//    y1 = v_rcp_f64(s) after one Newton step, e1 = 1 - s y1 (exact: fma),
+//    y1 = v_rcp_f64(s) after one Newton step, e1 = RN(1 - s y1) (fma),
 //    ylo = RN(e1 y1).  y1 + e1 y1 = (1 - e1^2) / s, so
 //        q = fma(n, y1, RN(n ylo))
-//    rounds n/s (1 - e1^2) + O(n/s |e1| 2^-53) once: |e1| <= 2^-52 + eps0^2
-//    (eps0 = the relative error of v_rcp_f64, far below 2^-14 on gfx950), so the
-//    value rounded is within 2^-50 ulp of n/s and q is a FAITHFUL rounding of
-//    n/s (one of its two neighbours), correctly rounded except when n/s lies
-//    within 2^-50 ulp of a rounding midpoint.
+//    rounds n/s (1 - e1^2) + O(n/s |e1| 2^-53) once.  dd_rcp also reports
+//    whether |e1| <= 2^-46 (ok; v_rcp_f64 alone is far more accurate, so this
+//    never fails in practice, but the proof below does not rely on its
+//    accuracy): then the value rounded is within 2^-90 relative of n/s and q
+//    is a FAITHFUL rounding of n/s (one of its two neighbours).
 //    The check: r = fma(-q, s, n) is exact (q faithful; n = 0 or n >= 2^-969,
-//    s and q normal), and with k = y1 (1 + 2^-30) >= (1 + 2^-31) / s
-//    (|1 - s y1| = |e1| <= 2^-51), r k = (n/s - q)(1 + kappa) exactly inside
-//        t = fma(r, k, q) = RN(q + (n/s - q) (1 + kappa)),  2^-31 <= kappa <= 2^-29
-//    (the default form t = fma(RN(r (1 + 2^-30)), y1, q) has the same bound:
-//    the extra rounding multiplies 1 + kappa by 1 + delta, |delta| <= 2^-53).
-//    If q != RN(n/s), |n/s - q| exceeds half the gap g between q and its
-//    neighbour towards n/s (g = ulp(q), or ulp(q)/2 below a power of two; n/s
-//    is never exactly a midpoint: s times a 54-bit odd significand has more
-//    than 53 bits), so q + (n/s - q)(1 + kappa) lies beyond that midpoint and
-//    t != q.  Contrapositive: t == q proves q == RN(n/s).  A correct q is
-//    flagged only when n/s lies within ~2^-30 ulp of a midpoint (probability
-//    ~2^-29 per quotient); the caller then redoes the work with div_rn.
-//    Cost per normalisation pair: 6 shared + 5 per quotient (the unchecked
-//    hipcc-sequence form was 5 + 3).
+//    s and q normal), r = s (n/s - q).  With r' = RN(r (1 + 2^-45)),
+//        t = fma(r', y1, q) = RN(q + (n/s - q) F),
+//        F = s y1 (1 + 2^-45)(1 + eps) = (1 - e1)(1 + 2^-45)(1 + eps) > 1
+//    (|eps| <= 2^-52 also when r' is subnormal: |r| >= 2^-1023 whenever q is
+//    not RN(n/s), below), and F < 1 + 2^-43.  If q != RN(n/s), |n/s - q|
+//    exceeds half the gap g between q and its neighbour towards n/s (g = ulp(q),
+//    or ulp(q)/2 below a power of two; n/s is never exactly a midpoint: s times
+//    a 54-bit odd significand has more than 53 bits), so q + (n/s - q) F lies
+//    strictly beyond that midpoint and t != q.  Contrapositive: ok and t == q
+//    prove q == RN(n/s).  A correct q is flagged only when n/s lies within
+//    2^-43 of half a gap from the midpoint (round 2 of this check used
+//    1 + 2^-30, flagging 2^13 times as many: a quarter of the BG2 codewords,
+//    whose saturated messages repeat the same few quotients, were redone).
+//    The caller then redoes the work with div_rn.
+//    Cost per normalisation pair: 6 shared + 1 compare + 5 per quotient.
 //
 // 2. div_rn (every other division: the decoders' exact re-decode, the
 //    non-FAST demap, k-means): any operands.  Finite normal operands with
@@ -52,40 +53,23 @@
 
 namespace kml {
 
-// KML_DD_CHECK_K (A/B): 1 = k = y1 (1 + 2^-30) kept per reciprocal (one mul
-// per pair, two more live registers per pair in flight); 0 = the residual
-// scaled by 1 + 2^-30 per quotient (one mul per quotient, no register).  The
-// same proof: r (1 + 2^-30) y1 = (n/s - q)(1 + 2^-30) s y1.
-#ifndef KML_DD_CHECK_K
-#define KML_DD_CHECK_K 0
-#endif
 struct DdRcp {
   double hi, lo;  // y1, RN(e1 y1)
-#if KML_DD_CHECK_K
-  double k;  // y1 (1 + 2^-30)
-#endif
+  bool ok;        // |e1| <= 2^-46: the premise of dd_check's proof
 };
 
 __device__ __forceinline__ DdRcp dd_rcp(double s) {
   const double y0 = __builtin_amdgcn_rcp(s);
   const double y1 = fma(y0, fma(-y0, s, 1.0), y0);
   const double e1 = fma(-y1, s, 1.0);
-#if KML_DD_CHECK_K
-  return {y1, e1 * y1, y1 * (1.0 + 0x1p-30)};
-#else
-  return {y1, e1 * y1};
-#endif
+  return {y1, e1 * y1, fabs(e1) <= 0x1p-46};
 }
 
 __device__ __forceinline__ double dd_quot(double n, const DdRcp &y) { return fma(n, y.hi, n * y.lo); }
 
-// true when q == RN(n / s) is proven (see 1. above)
+// true when q == RN(n / s) is proven, given y.ok (see 1. above)
 __device__ __forceinline__ bool dd_check(double n, double s, double q, const DdRcp &y) {
-#if KML_DD_CHECK_K
-  return fma(fma(-q, s, n), y.k, q) == q;
-#else
-  return fma(fma(-q, s, n) * (1.0 + 0x1p-30), y.hi, q) == q;
-#endif
+  return fma(fma(-q, s, n) * (1.0 + 0x1p-45), y.hi, q) == q;
 }
 
 // Integer long division for finite nonzero n, s (any magnitude): RN(n / s).

@@ -13,17 +13,20 @@ if [ "${TESTS:-0}" = 1 ]; then
 fi
 for r in 1 2; do
   for w in ${WORKLOADS:-headline}; do
+    E=""
     case $w in
       headline) A="" ;;
       blind) A="--blind" ;;
       bg2) A="--matrix 5GLDPCBG2a3_R12_K960.txt --modem 4bit_16QAM_Gray.txt --is5g --snr 5.01 --max-iter 50 --batch 16384 --steps 5" ;;
       peg8064) A="--matrix PEG8064regular0.5.txt --modem 6bits_64QAM_Gray.txt --snr 6.77 --blind --batch 4096 --steps 3" ;;
+      peg8064_512) A="--matrix PEG8064regular0.5.txt --modem 6bits_64QAM_Gray.txt --snr 6.77 --blind --batch 4096 --steps 3"; E="KML_PART=512" ;;
+      peg8064_768) A="--matrix PEG8064regular0.5.txt --modem 6bits_64QAM_Gray.txt --snr 6.77 --blind --batch 4096 --steps 3"; E="KML_PART=768" ;;
       *) echo "unknown workload $w"; exit 2 ;;
     esac
     for l in ${LIBS:-main}; do
       if [ "$l" = main ]; then L=kmldpc_amd/libkmldpc_amd.so; else L=kmldpc_amd/libkmldpc_amd_$l.so; fi
-      KML_LIB=$L timeout -k 10 200 python bench.py $A --no-cpu-baseline --no-ber-match --full-loop-batches 0 > $O/${w}_${l}_$r.json 2> $O/${w}_${l}_$r.err || exit $?
-      python3 -c "import json,sys; d=json.loads(open('$O/${w}_${l}_$r.json').read().strip().splitlines()[-1]); print('$w $l $r', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['stats'].get('stage_ms_per_step'))" >> $O/summary.txt
+      env $E KML_LIB=$L timeout -k 10 200 python bench.py $A --no-cpu-baseline --no-ber-match --full-loop-batches 0 > $O/${w}_${l}_$r.json 2> $O/${w}_${l}_$r.err || exit $?
+      python3 -c "import json,sys; d=json.loads(open('$O/${w}_${l}_$r.json').read().strip().splitlines()[-1]); print('$w $l $r', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['stats'].get('stage_ms_per_step'), 'redone', d['stats'].get('redone'))" >> $O/summary.txt
     done
   done
 done
