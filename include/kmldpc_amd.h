@@ -293,12 +293,12 @@ int kml_math_probe(kml_ctx *ctx, const double *in, int n, double *out);
 /* Device-side probe of the soft metric's log (kml_log, glibc-exact): out[i] = log(in[i]). */
 int kml_log_probe(kml_ctx *ctx, const double *in, int n, double *out);
 /* Device-side probe of the decoder's divisions (exact_div.hpp, bp_common.hpp):
- * in[n][3] = (n0, n1, s) -> out[n][11] = (FAST VN quotients n0/s, n1/s
+ * in[n][3] = (n0, n1, s) -> out[n][12] = (FAST VN quotients n0/s, n1/s
  * (dd_quot), div_rn n0/s, n1/s (correctly rounded, any operands), the CN
  * phase's near-one quotients n0/s, n1/s, the near-one reciprocal formula of s,
  * hipcc's refined reciprocal of s, hipcc's '/' n0/s, n1/s, flags: bit 0 / 1 =
  * dd_check could not prove the FAST quotient of n0 / n1, bit 2 = div2's
- * suspect flag). */
+ * suspect flag, |1 - s v_rcp_f64(s)|: the hardware reciprocal's error). */
 int kml_div_probe(kml_ctx *ctx, const double *in, int n, double *out);
 /* Test hook: after the nth (0-based) cooperative BP launch from now, set that
  * kernel's abort word as a timed-out group barrier would (nth < 0: off).  The

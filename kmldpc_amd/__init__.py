@@ -391,7 +391,7 @@ class Context:
 
     def div_probe(self, x):
         x = _f64(x).reshape(-1, 3)
-        out = np.zeros((x.shape[0], 11))
+        out = np.zeros((x.shape[0], 12))
         self._chk(lib().kml_div_probe(self._h, _p(x), x.shape[0], _p(out)), "kml_div_probe")
         return out
 

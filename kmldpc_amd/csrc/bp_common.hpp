@@ -168,6 +168,53 @@ __device__ __forceinline__ void cn_norm_rows(const double (&n0)[R], const double
 //     above 2^-961 and every sum and quotient normal ("Division"),
 //     inside dd_check's domain.
 //   !FAST: div_rn (any operands).
+// Diagnostic build (-DKML_DIV_STATS=1, `make variant`): counts of the FAST
+// VN divisions' failed premises and checks per translation unit, and the
+// operands of the first 64 failures ([0] pairs seen (per wave), [1] !ok,
+// [2] q0 unproven, [3] q1 unproven, [4] max |e1| bits, [8 + 5 i ..] samples:
+// n0, n1, s, q0, q1).  Read by kml_debug_div_stats.
+#ifndef KML_DIV_STATS
+#define KML_DIV_STATS 0
+#endif
+#if KML_DIV_STATS
+static __device__ unsigned long long kml_div_stats[8 + 5 * 64];
+__device__ __noinline__ void div_stats_record(bool ok, bool c0, bool c1, double n0, double n1, double s, double q0,
+                                              double q1) {
+  const unsigned long long all = __ballot(1), bok = __ballot(!ok), b0 = __ballot(!c0), b1 = __ballot(!c1);
+  if ((threadIdx.x & 63) == __builtin_ctzll(all)) {
+    atomicAdd(&kml_div_stats[0], (unsigned long long)__popcll(all));
+    if (bok) atomicAdd(&kml_div_stats[1], (unsigned long long)__popcll(bok));
+    if (b0) atomicAdd(&kml_div_stats[2], (unsigned long long)__popcll(b0));
+    if (b1) atomicAdd(&kml_div_stats[3], (unsigned long long)__popcll(b1));
+  }
+  {
+    const DdRcp y = dd_rcp(s);
+    const double e = fabs(fma(-y.hi, s, 1.0));
+    atomicMax(&kml_div_stats[4], (unsigned long long)__double_as_longlong(e));
+  }
+  if (!(ok & c0 & c1)) {
+    const unsigned long long i = atomicAdd(&kml_div_stats[5], 1ull);
+    if (i < 64) {
+      double *d = reinterpret_cast<double *>(&kml_div_stats[8 + 5 * i]);
+      d[0] = n0;
+      d[1] = n1;
+      d[2] = s;
+      d[3] = q0;
+      d[4] = q1;
+    }
+  }
+}
+#define KML_DIV_STATS_ACCESSOR(NAME)                                                                   \
+  extern "C" int NAME(unsigned long long *out, int reset) {                                            \
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(kml::kml_div_stats), sizeof(kml::kml_div_stats)); \
+    if (reset) {                                                                                       \
+      static unsigned long long zero[8 + 5 * 64];                                                      \
+      hipMemcpyToSymbol(HIP_SYMBOL(kml::kml_div_stats), zero, sizeof(zero));                           \
+    }                                                                                                  \
+    return e == hipSuccess ? 0 : -1;                                                                   \
+  }
+#endif
+
 template <bool FAST, bool CN = false>
 __device__ __forceinline__ void div2(double n0, double n1, double s, double &q0, double &q1, bool &sus) {
   if constexpr (!FAST) {
@@ -181,7 +228,11 @@ __device__ __forceinline__ void div2(double n0, double n1, double s, double &q0,
     const DdRcp y = dd_rcp(s);
     q0 = dd_quot(n0, y);
     q1 = dd_quot(n1, y);
-    sus |= !((int)y.ok & (int)dd_check(n0, s, q0, y) & (int)dd_check(n1, s, q1, y));
+    const bool c0 = dd_check(n0, s, q0, y), c1 = dd_check(n1, s, q1, y);
+    sus |= !((int)c0 & (int)c1);
+#if KML_DIV_STATS
+    div_stats_record(true, c0, c1, n0, n1, s, q0, q1);
+#endif
   }
 }
 // the CN phase's form (near-one sums: nothing to prove at run time)

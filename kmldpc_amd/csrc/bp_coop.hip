@@ -996,24 +996,21 @@ __device__ __forceinline__ int part_iterations_tagged(
 #else
       __builtin_amdgcn_s_setprio(3);
 #endif
-      double c0s[RV][DV];
-#pragma unroll
-      for (int r = 0; r < RV; ++r)
-#pragma unroll
-        for (int k = 0; k < DV; ++k)
-          c0s[r][k] = *reinterpret_cast<const double *>(smem + (vaddr[r][k] & 0xFFFF) * 16);
       // one column's chains at a time (column-major): the FAST divisions'
       // proofs keep a normalisation's operands live, and interleaving the RV
       // columns step by step doubled the live set (scratch spills in the loop)
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
+        double c0c[DV];  // the column's c2v, loaded per column (registers)
+#pragma unroll
+        for (int k = 0; k < DV; ++k) c0c[k] = *reinterpret_cast<const double *>(smem + (vaddr[r][k] & 0xFFFF) * 16);
         double a0 = pv[r], a1 = 1.0 - pv[r], al0[DV], al1[DV];
         unsigned hdb = 0;
 #pragma unroll
         for (int k = 0; k < DV; ++k) {
           al0[k] = a0;
           al1[k] = a1;
-          const double c0 = c0s[r][k];
+          const double c0 = c0c[k];
           const double n0 = a0 * c0;
           const double n1 = a1 * (1.0 - c0);
           if (k + 1 < DV) {
@@ -1046,7 +1043,7 @@ __device__ __forceinline__ int part_iterations_tagged(
             }
           }
           if (k > 0) {
-            const double c0 = c0s[r][k];
+            const double c0 = c0c[k];
             if (unit) {
               b0 = c0;
               b1 = 1.0 - c0;
@@ -1724,3 +1721,7 @@ bool bp_coop_aborted(const BpLaunch &a, int groups, hipStream_t s) {
 }
 
 }  // namespace kml
+
+#if KML_DIV_STATS
+KML_DIV_STATS_ACCESSOR(kml_debug_div_stats_coop)
+#endif

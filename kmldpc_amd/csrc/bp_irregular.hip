@@ -589,3 +589,7 @@ extern "C" int kml_debug_irr_stamps(unsigned long long *out, int reset) {
   return e == hipSuccess ? 0 : -3;
 }
 #endif
+
+#if KML_DIV_STATS
+KML_DIV_STATS_ACCESSOR(kml_debug_div_stats_irr)
+#endif

@@ -114,6 +114,9 @@ __device__ __forceinline__ double with_sign(double x, int bit) {
 // before that iteration's syndromes are written, so everything a suspect
 // decode wrote (slots, decisions, syndromes of earlier iterations) is what the
 // exact decode rewrites identically or overwrites.
+#ifndef KML_REG_VN_COLMAJOR
+#define KML_REG_VN_COLMAJOR 1
+#endif
 template <int T, int RV, int RC, int DV, int DC, bool SYN, bool FAST>
 __device__ __forceinline__ bool decode_reg(const DevCode &c, const BpLaunch &a, int cw, unsigned char *smem,
                                            unsigned hd, const unsigned (&vaddr)[RV][DV], const double (&pv)[RV],
@@ -156,6 +159,53 @@ __device__ __forceinline__ bool decode_reg(const DevCode &c, const BpLaunch &a, 
       for (int r = 0; r < RV; ++r)
 #pragma unroll
         for (int k = 0; k < DV; ++k) c0s[r][k] = iter == 0 ? 0.5 : lds_ld<double>(vaddr[r][k]);
+#if KML_REG_VN_COLMAJOR
+      // one column's chains at a time (registers: see bp_coop.hip)
+#pragma unroll
+      for (int r = 0; r < RV; ++r) {
+        double a0 = pv[r], a1 = 1.0 - pv[r], al0[DV], al1[DV];
+        int hb = 0;
+#pragma unroll
+        for (int k = 0; k < DV; ++k) {
+          al0[k] = a0;
+          al1[k] = a1;
+          const double c0 = c0s[r][k];
+          const double n0 = a0 * c0;
+          const double n1 = a1 * (1.0 - c0);
+          if (k + 1 < DV)
+            div2<FAST>(n0, n1, n0 + n1, a0, a1, sus);
+          else {  // the posterior only feeds the hard decision
+            hb = hard_decision<FAST>(n0, n1, sus);
+            lds_st<unsigned char>(hd + r * T, (unsigned char)hb);
+          }
+        }
+        if (r == RV / 2) __builtin_amdgcn_s_setprio(1);
+        double b0 = 1.0, b1 = 1.0;
+#pragma unroll
+        for (int k = DV - 1; k >= 0; --k) {
+          const bool unit = FAST && k == DV - 1;  // beta = (1, 1)
+          const double t0 = unit ? al0[k] : al0[k] * b0;
+          const double t1 = unit ? al1[k] : al1[k] * b1;
+          double q0, q1;
+          if (unit)
+            div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
+          else
+            div2<FAST>(t0, t1, t0 + t1, q0, q1, sus);
+          lds_st<dbl2>(vaddr[r][k] & ~15u, dbl2{q0, with_sign(q1, hb)});
+          if (k > 0) {
+            const double c0 = c0s[r][k];
+            if (unit) {
+              b0 = c0;
+              b1 = 1.0 - c0;
+            } else {
+              div2<FAST>(b0 * c0, b1 * (1.0 - c0), b0 * c0 + b1 * (1.0 - c0), b0, b1, sus);
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+#else
       double a0[RV], a1[RV], al0[RV][DV], al1[RV][DV];
       int hb[RV];
 #pragma unroll
@@ -216,6 +266,7 @@ __device__ __forceinline__ bool decode_reg(const DevCode &c, const BpLaunch &a, 
         }
       }
     }
+#endif
     REG_WSTAMP(0);
     __syncthreads();
     REG_WSTAMP(1);
@@ -639,3 +690,7 @@ bool bp_regular_fuses_demap(const DevCode &c, int bits) {
 }
 
 }  // namespace kml
+
+#if KML_DIV_STATS
+KML_DIV_STATS_ACCESSOR(kml_debug_div_stats_reg)
+#endif

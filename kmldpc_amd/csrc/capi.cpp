@@ -1663,9 +1663,9 @@ int kml_div_probe(kml_ctx *c, const double *in, int n, double *out) {
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
   const double *d_in;
   TRY(stage_in(c, c->w_y, in, (size_t)n * 3, 0, d_in));
-  HIPCHK(c, c->w_p0.ensure(sizeof(double) * 11 * (size_t)n), "hipMalloc");
+  HIPCHK(c, c->w_p0.ensure(sizeof(double) * 12 * (size_t)n), "hipMalloc");
   HIPCHK(c, kml::launch_div_probe(d_in, n, c->w_p0.as<double>(), c->stream), "div probe");
-  TRY(copy_out(c, out, (const double *)c->w_p0.as<double>(), (size_t)n * 11, 0));
+  TRY(copy_out(c, out, (const double *)c->w_p0.as<double>(), (size_t)n * 12, 0));
   return sync(c);
 }
 

@@ -22,7 +22,7 @@ __device__ __forceinline__ double prob_clip(double v) {  // utility.cc:18-26
 // then reruns the symbol on the exact path.
 __device__ __forceinline__ double qdiv(double n, double s, const DdRcp &r, bool &ok) {
   const double q = dd_quot(n, r);
-  ok &= r.ok & dd_check(n, s, q, r);
+  ok &= dd_check(n, s, q, r);
   return q;
 }
 
@@ -139,7 +139,7 @@ __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double 
     const double qk = FAST ? qdiv(pr[k], sum, rs, ok_k) : div_rn(pr[k], sum);
     // a faithful quotient below 1e-12 has RN's clip: RN is it or its upper
     // neighbour, at most 1e-12 (terms below 2^-969, outside the check's domain)
-    if (FAST) dok &= rs.ok & (ok_k | (qk < kSmallestProb));  // faithful needs rs.ok
+    if (FAST) dok &= ok_k | (qk < kSmallestProb);
     pr[k] = prob_clip(prob_clip(qk));
     pr[k] = w * pr[k];
     sum2 += pr[k];

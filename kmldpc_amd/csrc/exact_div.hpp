@@ -10,30 +10,32 @@
 // provably RN(n / s).
 //
 // 1. dd_quot + dd_check (the decoders' FAST VN divisions, demap_common.hpp):
-//    y1 = v_rcp_f64(s) after one Newton step, e1 = RN(1 - s y1) (fma),
-//    ylo = RN(e1 y1).  y1 + e1 y1 = (1 - e1^2) / s, so
+//    y0 = v_rcp_f64(s), whose relative error e0 the ISA documents as at most
+//    2^29 ulp = 2^-23 (tests/test_gpu_parity.py::test_fast_division_* measures
+//    it on the device); y1 = y0 after one Newton step, e1 = RN(1 - s y1)
+//    (fma), |e1| <= e0^2 + 2^-53 < 2^-45; ylo = RN(e1 y1).
+//    y1 + e1 y1 = (1 - e1^2) / s, so
 //        q = fma(n, y1, RN(n ylo))
-//    rounds n/s (1 - e1^2) + O(n/s |e1| 2^-53) once.  dd_rcp also reports
-//    whether |e1| <= 2^-46 (ok; v_rcp_f64 alone is far more accurate, so this
-//    never fails in practice, but the proof below does not rely on its
-//    accuracy): then the value rounded is within 2^-90 relative of n/s and q
-//    is a FAITHFUL rounding of n/s (one of its two neighbours).
+//    rounds a value within 2^-90 relative of n/s once: q is a FAITHFUL
+//    rounding of n/s (one of its two neighbours).  (The argument needs only
+//    |e1| <= 2^-30, i.e. e0 <= 2^-15: 2^8 below the documented bound.)
 //    The check: r = fma(-q, s, n) is exact (q faithful; n = 0 or n >= 2^-969,
-//    s and q normal), r = s (n/s - q).  With r' = RN(r (1 + 2^-45)),
-//        t = fma(r', y1, q) = RN(q + (n/s - q) F),
-//        F = s y1 (1 + 2^-45)(1 + eps) = (1 - e1)(1 + 2^-45)(1 + eps) > 1
-//    (|eps| <= 2^-52 also when r' is subnormal: |r| >= 2^-1023 whenever q is
-//    not RN(n/s), below), and F < 1 + 2^-43.  If q != RN(n/s), |n/s - q|
-//    exceeds half the gap g between q and its neighbour towards n/s (g = ulp(q),
-//    or ulp(q)/2 below a power of two; n/s is never exactly a midpoint: s times
-//    a 54-bit odd significand has more than 53 bits), so q + (n/s - q) F lies
-//    strictly beyond that midpoint and t != q.  Contrapositive: ok and t == q
-//    prove q == RN(n/s).  A correct q is flagged only when n/s lies within
-//    2^-43 of half a gap from the midpoint (round 2 of this check used
-//    1 + 2^-30, flagging 2^13 times as many: a quarter of the BG2 codewords,
-//    whose saturated messages repeat the same few quotients, were redone).
-//    The caller then redoes the work with div_rn.
-//    Cost per normalisation pair: 6 shared + 1 compare + 5 per quotient.
+//    s and q normal), r = s (n/s - q).  d = fma(r, y1, RN(r ylo)) is
+//    (n/s - q)(1 + theta), |theta| <= 2^-53 + 2^-88 (s (y1 + ylo) = 1 - e1^2;
+//    the roundings of r ylo, of e1 and of d), and
+//        t = fma(d, 1 + 2^-49, q) = RN(q + (n/s - q) F),  F = (1 + theta)(1 + 2^-49),
+//    so 1 < F < 1 + 2^-48.  (On the FAST path n/s >= 2^-962: d stays normal
+//    whenever q is not RN(n/s).)  If q != RN(n/s), |n/s - q| exceeds half the
+//    gap g between q and its neighbour towards n/s (g = ulp(q), or ulp(q)/2
+//    below a power of two; n/s is never exactly a midpoint: s times a 54-bit
+//    odd significand has more than 53 bits), so q + (n/s - q) F lies strictly
+//    beyond that midpoint and t != q.  Contrapositive: t == q proves
+//    q == RN(n/s).  A correct q is flagged only when n/s lies within 2^-48 of
+//    half a gap from the midpoint, and the caller then redoes the work with
+//    div_rn.  (The first form of this check scaled r by 1 + 2^-30 and relied
+//    on nothing about e1 beyond that: it flagged 2^18 times as often, which on
+//    BG2 redid a quarter of the codewords.)
+//    Cost per normalisation pair: 6 shared + 6 per quotient.
 //
 // 2. div_rn (every other division: the decoders' exact re-decode, the
 //    non-FAST demap, k-means): any operands.  Finite normal operands with
@@ -55,21 +57,21 @@ namespace kml {
 
 struct DdRcp {
   double hi, lo;  // y1, RN(e1 y1)
-  bool ok;        // |e1| <= 2^-46: the premise of dd_check's proof
 };
 
 __device__ __forceinline__ DdRcp dd_rcp(double s) {
   const double y0 = __builtin_amdgcn_rcp(s);
   const double y1 = fma(y0, fma(-y0, s, 1.0), y0);
   const double e1 = fma(-y1, s, 1.0);
-  return {y1, e1 * y1, fabs(e1) <= 0x1p-46};
+  return {y1, e1 * y1};
 }
 
 __device__ __forceinline__ double dd_quot(double n, const DdRcp &y) { return fma(n, y.hi, n * y.lo); }
 
-// true when q == RN(n / s) is proven, given y.ok (see 1. above)
+// true when q == RN(n / s) is proven (see 1. above)
 __device__ __forceinline__ bool dd_check(double n, double s, double q, const DdRcp &y) {
-  return fma(fma(-q, s, n) * (1.0 + 0x1p-45), y.hi, q) == q;
+  const double r = fma(-q, s, n);
+  return fma(fma(r, y.hi, r * y.lo), 1.0 + 0x1p-49, q) == q;
 }
 
 // Integer long division for finite nonzero n, s (any magnitude): RN(n / s).

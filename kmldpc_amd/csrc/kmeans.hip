@@ -1123,9 +1123,9 @@ __global__ void div_probe_kernel(const double *in, int n, double *out) {
   bool sus = false;
   div2<true>(n0, n1, s, q0, q1, sus);  // the FAST VN form: dd_quot + dd_check
   const DdRcp y = dd_rcp(s);
-  const int flags = (y.ok && dd_check(n0, s, q0, y) ? 0 : 1) | (y.ok && dd_check(n1, s, q1, y) ? 0 : 2);
+  const int flags = (dd_check(n0, s, q0, y) ? 0 : 1) | (dd_check(n1, s, q1, y) ? 0 : 2);
   div2<true, true>(n0, n1, s, c0, c1);
-  double *o = out + 11 * (long long)i;
+  double *o = out + 12 * (long long)i;
   o[0] = q0;
   o[1] = q1;
   o[2] = div_rn(n0, s);
@@ -1137,6 +1137,7 @@ __global__ void div_probe_kernel(const double *in, int n, double *out) {
   o[8] = n0 / s;  // hipcc's '/'
   o[9] = n1 / s;
   o[10] = (double)(flags | (sus ? 4 : 0));
+  o[11] = fabs(fma(-__builtin_amdgcn_rcp(s), s, 1.0));  // e0 (exact_div.hpp: documented <= 2^-23)
 }
 }  // namespace
 
