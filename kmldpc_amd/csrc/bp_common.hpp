@@ -161,8 +161,11 @@ __device__ __forceinline__ void cn_norm_rows(const double (&n0)[R], const double
 //     unit-beta step): the near-one reciprocal and the division tail, exact by
 //     exhaustive enumeration (rcp_near1).
 //   FAST, VN: exact_div.hpp dd_quot — faithful always, and proven correctly
-//     rounded by dd_check; a quotient the check cannot prove sets sus, and the
-//     caller redoes the codeword on the exact path (FAST = false).  The FAST
+//     rounded by dd_check; a quotient the check cannot prove (n/s next to a
+//     rounding midpoint: rare, but BP's saturated messages repeat such
+//     quotients) is settled by dd_fix, its neighbour's exact residual.  So
+//     every FAST VN quotient is RN(n/s) and sus stays as the caller set it
+//     (div2 keeps the flag for the kernels' redo machinery).  The FAST
 //     path runs only for codewords whose priors pass fast_prior_ok (on codes
 //     with column degree <= 23), which keeps every nonzero numerator at or
 //     above 2^-961 and every sum and quotient normal ("Division"),
@@ -229,10 +232,13 @@ __device__ __forceinline__ void div2(double n0, double n1, double s, double &q0,
     q0 = dd_quot(n0, y);
     q1 = dd_quot(n1, y);
     const bool c0 = dd_check(n0, s, q0, y), c1 = dd_check(n1, s, q1, y);
-    sus |= !((int)c0 & (int)c1);
 #if KML_DIV_STATS
     div_stats_record(true, c0, c1, n0, n1, s, q0, q1);
 #endif
+    if (__builtin_expect(!((int)c0 & (int)c1), 0)) {  // n/s within 2^-48 of a half gap from a midpoint: rare
+      if (!c0) q0 = dd_fix(n0, s, q0);
+      if (!c1) q1 = dd_fix(n1, s, q1);
+    }
   }
 }
 // the CN phase's form (near-one sums: nothing to prove at run time)

@@ -31,11 +31,13 @@
 //    odd significand has more than 53 bits), so q + (n/s - q) F lies strictly
 //    beyond that midpoint and t != q.  Contrapositive: t == q proves
 //    q == RN(n/s).  A correct q is flagged only when n/s lies within 2^-48 of
-//    half a gap from the midpoint, and the caller then redoes the work with
-//    div_rn.  (The first form of this check scaled r by 1 + 2^-30 and relied
-//    on nothing about e1 beyond that: it flagged 2^18 times as often, which on
-//    BG2 redid a quarter of the codewords.)
-//    Cost per normalisation pair: 6 shared + 6 per quotient.
+//    half a gap from the midpoint.  BP's saturated messages make such
+//    quotients recur (e.g. n0 = 1/4 + 3 ulp, s = 1/2 - 2^-55: n/s within
+//    2^-50 of a midpoint, measured by tools/div_stats.py), so the decoders
+//    settle a flagged quotient in place with dd_fix (q faithful: RN(n/s) is q
+//    or its neighbour, told apart by their exact residuals) instead of
+//    redoing the codeword; the demapper reruns the symbol on the exact path.
+//    Cost per normalisation pair: 6 shared + 6 per quotient (+ the fix, rare).
 //
 // 2. div_rn (every other division: the decoders' exact re-decode, the
 //    non-FAST demap, k-means): any operands.  Finite normal operands with
@@ -72,6 +74,16 @@ __device__ __forceinline__ double dd_quot(double n, const DdRcp &y) { return fma
 __device__ __forceinline__ bool dd_check(double n, double s, double q, const DdRcp &y) {
   const double r = fma(-q, s, n);
   return fma(fma(r, y.hi, r * y.lo), 1.0 + 0x1p-49, q) == q;
+}
+
+// RN(n / s) from a faithful q that dd_check could not prove: q or its
+// neighbour towards n / s, whichever has the smaller residual (both residuals
+// exact in dd_check's domain, |residual| = |s| * distance to n / s; no ties).
+__device__ __forceinline__ double dd_fix(double n, double s, double q) {
+  const double r = fma(-q, s, n);
+  const long long step = ((r > 0.0) == (s > 0.0)) == (q > 0.0) ? 1 : -1;
+  const double qn = __longlong_as_double(__double_as_longlong(q) + step);
+  return fabs(fma(-qn, s, n)) < fabs(r) ? qn : q;
 }
 
 // Integer long division for finite nonzero n, s (any magnitude): RN(n / s).
