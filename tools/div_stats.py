@@ -27,6 +27,9 @@ def as_f(u):
 
 def midpoint_gap(n, s, q):
     """(n/s - q) / half-gap towards n/s, exactly (1.0 = at the midpoint)."""
+    import math
+    if not all(math.isfinite(v) for v in (n, s, q)) or s == 0:
+        return None
     x = Fraction(n) / Fraction(s)
     fq = Fraction(q)
     import math
@@ -68,7 +71,9 @@ def main():
         samples = []
         for i in range(min(64, v[5])):
             n0, n1, s, q0, q1 = (as_f(x) for x in v[8 + 5 * i: 13 + 5 * i])
-            samples.append({"n0": n0.hex(), "n1": n1.hex(), "s": s.hex(), "q0_ok": q0 == n0 / s, "q1_ok": q1 == n1 / s,
+            ok0 = s != 0 and q0 == n0 / s
+            ok1 = s != 0 and q1 == n1 / s
+            samples.append({"n0": n0.hex(), "n1": n1.hex(), "s": s.hex(), "q0_ok": ok0, "q1_ok": ok1,
                             "g0": midpoint_gap(n0, s, q0), "g1": midpoint_gap(n1, s, q1)})
         out["tu"][n] = {"pairs": v[0], "rcp_premise_failed": v[1], "q0_unproven": v[2], "q1_unproven": v[3],
                         "max_abs_e1": as_f(v[4]), "failures": v[5], "samples": samples[:16]}
