@@ -11,8 +11,8 @@
 //
 // 1. dd_quot + dd_check (the decoders' FAST VN divisions, demap_common.hpp):
 //    y0 = v_rcp_f64(s), whose relative error e0 the ISA documents as at most
-//    2^29 ulp = 2^-23 (tests/test_gpu_parity.py::test_fast_division_* measures
-//    it on the device); y1 = y0 after one Newton step, e1 = RN(1 - s y1)
+//    2^29 ulp = 2^-23 (tests/test_gpu_parity.py::test_hardware_reciprocal_error
+//    measures it on the device); y1 = y0 after one Newton step, e1 = RN(1 - s y1)
 //    (fma), |e1| <= e0^2 + 2^-53 < 2^-45; ylo = RN(e1 y1).
 //    y1 + e1 y1 = (1 - e1^2) / s, so
 //        q = fma(n, y1, RN(n ylo))
@@ -20,24 +20,24 @@
 //    rounding of n/s (one of its two neighbours).  (The argument needs only
 //    |e1| <= 2^-30, i.e. e0 <= 2^-15: 2^8 below the documented bound.)
 //    The check: r = fma(-q, s, n) is exact (q faithful; n = 0 or n >= 2^-969,
-//    s and q normal), r = s (n/s - q).  d = fma(r, y1, RN(r ylo)) is
-//    (n/s - q)(1 + theta), |theta| <= 2^-53 + 2^-88 (s (y1 + ylo) = 1 - e1^2;
-//    the roundings of r ylo, of e1 and of d), and
-//        t = fma(d, 1 + 2^-49, q) = RN(q + (n/s - q) F),  F = (1 + theta)(1 + 2^-49),
-//    so 1 < F < 1 + 2^-48.  (On the FAST path n/s >= 2^-962: d stays normal
-//    whenever q is not RN(n/s).)  If q != RN(n/s), |n/s - q| exceeds half the
-//    gap g between q and its neighbour towards n/s (g = ulp(q), or ulp(q)/2
-//    below a power of two; n/s is never exactly a midpoint: s times a 54-bit
-//    odd significand has more than 53 bits), so q + (n/s - q) F lies strictly
-//    beyond that midpoint and t != q.  Contrapositive: t == q proves
-//    q == RN(n/s).  A correct q is flagged only when n/s lies within 2^-48 of
-//    half a gap from the midpoint.  BP's saturated messages make such
-//    quotients recur (e.g. n0 = 1/4 + 3 ulp, s = 1/2 - 2^-55: n/s within
-//    2^-50 of a midpoint, measured by tools/div_stats.py), so the decoders
-//    settle a flagged quotient in place with dd_fix (q faithful: RN(n/s) is q
-//    or its neighbour, told apart by their exact residuals) instead of
-//    redoing the codeword; the demapper reruns the symbol on the exact path.
-//    Cost per normalisation pair: 6 shared + 6 per quotient (+ the fix, rare).
+//    s and q normal), r = s (n/s - q).  With yk = RN(y1 (1 + 2^-40)),
+//        t = fma(r, yk, q) = RN(q + (n/s - q) F),  F = s yk = (1 - e1)(1 + 2^-40)(1 + eps),
+//    |eps| <= 2^-53, so 1 < F < 1 + 2^-39 whenever |e1| < 2^-40.1, i.e. e0 <=
+//    2^-20.1: 2^2.9 below the documented bound (the fma forms r yk exactly,
+//    and t rounds once).  If q != RN(n/s),
+//    |n/s - q| exceeds half the gap g between q and its neighbour towards n/s
+//    (g = ulp(q), or ulp(q)/2 below a power of two; n/s is never exactly a
+//    midpoint: s times a 54-bit odd significand has more than 53 bits), so
+//    q + (n/s - q) F lies strictly beyond that midpoint and t != q.
+//    Contrapositive: t == q proves q == RN(n/s).  A correct q is flagged only
+//    when n/s lies within 2^-39 of half a gap from the midpoint.  BP's
+//    saturated messages make such quotients recur (e.g. n0 = 1/4 + 3 ulp,
+//    s = 1/2 - 2^-55: n/s within 2^-50 of a midpoint, measured by
+//    tools/div_stats.py), so the decoders settle a flagged quotient in place
+//    with dd_fix (q faithful: RN(n/s) is q or its neighbour, told apart by
+//    their exact residuals) instead of redoing the codeword; the demapper
+//    reruns the symbol on the exact path.
+//    Cost per normalisation pair: 7 shared + 4 per quotient (+ the fix, rare).
 //
 // 2. div_rn (every other division: the decoders' exact re-decode, the
 //    non-FAST demap, k-means): any operands.  Finite normal operands with
@@ -70,10 +70,10 @@ __device__ __forceinline__ DdRcp dd_rcp(double s) {
 
 __device__ __forceinline__ double dd_quot(double n, const DdRcp &y) { return fma(n, y.hi, n * y.lo); }
 
-// true when q == RN(n / s) is proven (see 1. above)
+// true when q == RN(n / s) is proven (see 1. above); the two quotients of a
+// pair share yk (common subexpression)
 __device__ __forceinline__ bool dd_check(double n, double s, double q, const DdRcp &y) {
-  const double r = fma(-q, s, n);
-  return fma(fma(r, y.hi, r * y.lo), 1.0 + 0x1p-49, q) == q;
+  return fma(fma(-q, s, n), y.hi * (1.0 + 0x1p-40), q) == q;
 }
 
 // RN(n / s) from a faithful q that dd_check could not prove: q or its
@@ -142,16 +142,20 @@ __device__ __forceinline__ double div_soft(double n, double s) {
 }
 
 // RN(n / s) outside div_rn's fast domain: zeros, infinities and NaNs (IEEE
-// cases: hipcc's '/'), else the integer long division.  Out of line: it is
-// rare, and inlined at every division site it multiplied the exact kernels'
-// code size past the instruction cache.
-__device__ __noinline__ double div_rn_cold(double n, double s) {
+// cases: hipcc's '/'), else the integer long division.
+__device__ __forceinline__ double div_rn_rare(double n, double s) {
   const double an = fabs(n), as = fabs(s);
   if (!(an > 0.0) || !(as > 0.0) || an == INFINITY || as == INFINITY) return n / s;  // 0, inf, NaN: IEEE cases
   return div_soft(n, s);
 }
+// Out of line: inlined at every division site of the exact kernels it
+// multiplied their code size past the instruction cache.
+__device__ __noinline__ double div_rn_cold(double n, double s) { return div_rn_rare(n, s); }
 
-// RN(n / s) for any operands (see 2. above).
+// RN(n / s) for any operands (see 2. above).  INLINE_RARE: the rare path
+// inline too (a kernel with few division sites, where a call's register
+// convention would cost more than the code: k-means).
+template <bool INLINE_RARE = false>
 __device__ __forceinline__ double div_rn(double n, double s) {
   const double an = fabs(n), as = fabs(s);
   if (__builtin_expect((an >= 0x1p-969) & (an < 0x1p1000) & (as >= 0x1p-1000) & (as < 0x1p1000), 1)) {
@@ -167,7 +171,8 @@ __device__ __forceinline__ double div_rn(double n, double s) {
       return fabs(fma(-qn, s, n)) < fabs(r) ? qn : q;
     }
   }
-  return div_rn_cold(n, s);
+  if constexpr (INLINE_RARE) return div_rn_rare(n, s);
+  else return div_rn_cold(n, s);
 }
 
 }  // namespace kml

@@ -59,10 +59,11 @@
 namespace kml {
 
 // RN(a / b): the host's IEEE division, and on the device exact_div.hpp div_rn
-// (hipcc's f64 '/' is not correctly rounded everywhere).
+// (hipcc's f64 '/' is not correctly rounded everywhere), its rare path inline
+// (k-means: few division sites, and a call would raise its registers).
 KML_HD double kml_div(double a, double b) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return div_rn(a, b);
+  return div_rn<true>(a, b);
 #else
   return a / b;
 #endif

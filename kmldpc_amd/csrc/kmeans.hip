@@ -685,8 +685,11 @@ __device__ __forceinline__ cplx cdiv_const(cplx n, cplx dd, const CdivConst &k) 
   return cplx{x, y};
 }
 
+// four waves per SIMD (<= 128 registers): 7 codewords per CU fit the LDS, and
+// at 129+ registers only 6 do (QPSK: 3.3 -> 4.1 ms when the exact division's
+// registers pushed it past)
 template <int KC>
-__global__ __launch_bounds__(kFusedT) void km_fused_kernel(const double *__restrict__ cons,
+__global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8 ? 1 : 4))) void km_fused_kernel(const double *__restrict__ cons,
                                                            const double *__restrict__ rot,
                                                            const double2 *__restrict__ y, int S, int iters,
                                                            double2 *__restrict__ h_hat, double2 *__restrict__ h4,
