@@ -218,7 +218,10 @@ __device__ __noinline__ void div_stats_record(bool ok, bool c0, bool c1, double 
   }
 #endif
 
-template <bool FAST, bool CN = false>
+// DEFER (FAST VN only): a quotient the check cannot prove is left faithful and
+// sets sus, for a caller that then reruns the whole column with DEFER = false
+// (one rare branch per column instead of one per normalisation).
+template <bool FAST, bool CN = false, bool DEFER = false>
 __device__ __forceinline__ void div2(double n0, double n1, double s, double &q0, double &q1, bool &sus) {
   if constexpr (!FAST) {
     q0 = div_rn(n0, s);
@@ -235,7 +238,9 @@ __device__ __forceinline__ void div2(double n0, double n1, double s, double &q0,
 #if KML_DIV_STATS
     div_stats_record(true, c0, c1, n0, n1, s, q0, q1);
 #endif
-    if (__builtin_expect(!((int)c0 & (int)c1), 0)) {  // n/s within 2^-48 of a half gap from a midpoint: rare
+    if constexpr (DEFER) {
+      sus |= !((int)c0 & (int)c1);
+    } else if (__builtin_expect(!((int)c0 & (int)c1), 0)) {  // n/s next to a rounding midpoint: rare
       if (!c0) q0 = dd_fix(n0, s, q0);
       if (!c1) q1 = dd_fix(n1, s, q1);
     }

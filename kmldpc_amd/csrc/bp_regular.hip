@@ -37,6 +37,8 @@
 //   * every LDS address is kept absolute in a register (bp_common.hpp lds_ld).
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "bp_common.hpp"
 #include "demap_common.hpp"
 #include "kernels.hpp"
@@ -160,48 +162,57 @@ __device__ __forceinline__ bool decode_reg(const DevCode &c, const BpLaunch &a, 
 #pragma unroll
         for (int k = 0; k < DV; ++k) c0s[r][k] = iter == 0 ? 0.5 : lds_ld<double>(vaddr[r][k]);
 #if KML_REG_VN_COLMAJOR
-      // one column's chains at a time (registers: see bp_coop.hip)
+      // one column's chains at a time (registers: see bp_coop.hip).  FAST: the
+      // column's quotients unsettled (div2 DEFER), and in the rare case that
+      // one of them could not be proven the column runs again settling each
+      // (its slot and decision stores are rewritten before the barrier).
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
-        double a0 = pv[r], a1 = 1.0 - pv[r], al0[DV], al1[DV];
-        int hb = 0;
+        auto column = [&](auto defer) -> bool {
+          constexpr bool D = FAST && decltype(defer)::value;
+          bool bad = false;
+          double a0 = pv[r], a1 = 1.0 - pv[r], al0[DV], al1[DV];
+          int hb = 0;
 #pragma unroll
-        for (int k = 0; k < DV; ++k) {
-          al0[k] = a0;
-          al1[k] = a1;
-          const double c0 = c0s[r][k];
-          const double n0 = a0 * c0;
-          const double n1 = a1 * (1.0 - c0);
-          if (k + 1 < DV)
-            div2<FAST>(n0, n1, n0 + n1, a0, a1, sus);
-          else {  // the posterior only feeds the hard decision
-            hb = hard_decision<FAST>(n0, n1, sus);
-            lds_st<unsigned char>(hd + r * T, (unsigned char)hb);
-          }
-        }
-        if (r == RV / 2) __builtin_amdgcn_s_setprio(1);
-        double b0 = 1.0, b1 = 1.0;
-#pragma unroll
-        for (int k = DV - 1; k >= 0; --k) {
-          const bool unit = FAST && k == DV - 1;  // beta = (1, 1)
-          const double t0 = unit ? al0[k] : al0[k] * b0;
-          const double t1 = unit ? al1[k] : al1[k] * b1;
-          double q0, q1;
-          if (unit)
-            div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
-          else
-            div2<FAST>(t0, t1, t0 + t1, q0, q1, sus);
-          lds_st<dbl2>(vaddr[r][k] & ~15u, dbl2{q0, with_sign(q1, hb)});
-          if (k > 0) {
+          for (int k = 0; k < DV; ++k) {
+            al0[k] = a0;
+            al1[k] = a1;
             const double c0 = c0s[r][k];
-            if (unit) {
-              b0 = c0;
-              b1 = 1.0 - c0;
-            } else {
-              div2<FAST>(b0 * c0, b1 * (1.0 - c0), b0 * c0 + b1 * (1.0 - c0), b0, b1, sus);
+            const double n0 = a0 * c0;
+            const double n1 = a1 * (1.0 - c0);
+            if (k + 1 < DV)
+              div2<FAST, false, D>(n0, n1, n0 + n1, a0, a1, bad);
+            else {  // the posterior only feeds the hard decision
+              hb = hard_decision<FAST>(n0, n1, sus);
+              lds_st<unsigned char>(hd + r * T, (unsigned char)hb);
             }
           }
-        }
+          double b0 = 1.0, b1 = 1.0;
+#pragma unroll
+          for (int k = DV - 1; k >= 0; --k) {
+            const bool unit = FAST && k == DV - 1;  // beta = (1, 1)
+            const double t0 = unit ? al0[k] : al0[k] * b0;
+            const double t1 = unit ? al1[k] : al1[k] * b1;
+            double q0, q1;
+            if (unit)
+              div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
+            else
+              div2<FAST, false, D>(t0, t1, t0 + t1, q0, q1, bad);
+            lds_st<dbl2>(vaddr[r][k] & ~15u, dbl2{q0, with_sign(q1, hb)});
+            if (k > 0) {
+              const double c0 = c0s[r][k];
+              if (unit) {
+                b0 = c0;
+                b1 = 1.0 - c0;
+              } else {
+                div2<FAST, false, D>(b0 * c0, b1 * (1.0 - c0), b0 * c0 + b1 * (1.0 - c0), b0, b1, bad);
+              }
+            }
+          }
+          return bad;
+        };
+        if (column(std::true_type{})) column(std::false_type{});
+        if (r == RV / 2) __builtin_amdgcn_s_setprio(1);
       }
       __builtin_amdgcn_s_setprio(0);
     }
