@@ -581,6 +581,9 @@ def main():
         line["cpu_baseline"] = cpu_baseline(d, args)
     print(json.dumps(line), flush=True)
     ctx.close()  # release the device buffers while the runtime is fully up
+    if os.environ.get("KML_DUMP_MAPS"):  # diagnostics: map a crash at exit to its library
+        with open("/proc/self/maps") as src, open(os.environ["KML_DUMP_MAPS"], "w") as dst:
+            dst.write(src.read())
     if dist is not None:
         dist.destroy_process_group()
 

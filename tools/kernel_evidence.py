@@ -80,8 +80,8 @@ def per_launch(cnt, fam):
     out = {}
     for c in names:
         tot = sum(v[c][0] for v in vs.values() if c in v)
-        if fam in BP_FAMILIES:
-            n = vs.get("exact", {}).get(c, (0, 0))[1]
+        if fam in BP_FAMILIES and "exact" in vs:
+            n = vs["exact"].get(c, (0, 0))[1]
         else:
             n = sum(v[c][1] for v in vs.values() if c in v)
         if n:
