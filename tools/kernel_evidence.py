@@ -10,7 +10,8 @@ EXACT kernel over the codewords the FAST one deferred (kernels.hpp; one EXACT
 dispatch per chain, usually with no work).  bench.py's avg_launch_ms times the
 whole chain (one kml run_bp), so every BP figure here is per chain: the
 family's total duration and counter totals over the run / its EXACT dispatches.
-Other kernels: per dispatch.
+demap_kernel and cand_metric_kernel are FAST + EXACT pairs too.  Other kernels:
+per dispatch.
 
 Per kernel: average duration, HBM bytes ((2*FETCH_SIZE + WRITE_SIZE) KiB x
 1024, the gfx950 FETCH_SIZE half-count correction of MI355X_MICROARCH.md) and
@@ -33,6 +34,8 @@ from collections import defaultdict
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6
 BP_FAMILIES = ("bp_regular_kernel", "bp_irregular_kernel", "bp_coop_kernel", "bp_part_kernel")
+# kernels launched as a FAST dispatch + an EXACT dispatch over its deferrals (last template argument EXACT)
+CHAIN_FAMILIES = BP_FAMILIES + ("demap_kernel", "cand_metric_kernel")
 # resident waves per SIMD of each kernel family (block size / register limits)
 WAVES_PER_SIMD = {"bp_regular_kernel": 3, "bp_irregular_kernel": 3, "bp_part_kernel": 4}
 
@@ -41,7 +44,7 @@ def parse(name):
     """(family, variant) of a rocprofv3 kernel name; variant 'exact' marks a chain's last dispatch."""
     n = name.replace("kml::(anonymous namespace)::", "").replace("void ", "")
     fam = n.split("(")[0].split("<")[0].strip()
-    if fam not in BP_FAMILIES or "<" not in n:
+    if fam not in CHAIN_FAMILIES or "<" not in n:
         return fam, ""
     targs = [t.strip() for t in n.split("<", 1)[1].split(">")[0].split(",")]
     exact = targs[-1] == "true"
@@ -80,7 +83,7 @@ def per_launch(cnt, fam):
     out = {}
     for c in names:
         tot = sum(v[c][0] for v in vs.values() if c in v)
-        if fam in BP_FAMILIES and "exact" in vs:
+        if fam in CHAIN_FAMILIES and "exact" in vs:
             n = vs["exact"].get(c, (0, 0))[1]
         else:
             n = sum(v[c][1] for v in vs.values() if c in v)
@@ -95,13 +98,13 @@ def evidence(d):
     out = {}
     for fam, vs in sorted(dur.items(), key=lambda kv: -sum(x[1] for x in kv[1].values())):
         total_ns = sum(x[1] for x in vs.values())
-        if fam in BP_FAMILIES:
+        if fam in CHAIN_FAMILIES:
             launches = vs.get("exact", [0, 0.0])[0] or sum(x[0] for x in vs.values())
         else:
             launches = sum(x[0] for x in vs.values())
         ms = total_ns / max(launches, 1) / 1e6
         e = {"launches": launches, "avg_ms": round(ms, 4)}
-        if fam in BP_FAMILIES:
+        if fam in CHAIN_FAMILIES:
             e["per"] = "launch chain (FAST dispatches + the EXACT dispatch)"
             e["dispatches"] = {v: {"calls": x[0], "avg_ms": round(x[1] / max(x[0], 1) / 1e6, 4)} for v, x in vs.items()}
         c = per_launch(cnt, fam)
