@@ -256,8 +256,9 @@ __global__ void km_final_kernel(const double *__restrict__ cons, const double *_
 // their values onto the cumulative sum in that order (the reference's
 // sequential rounding: wave 0 the real chain, wave 1 the imaginary chain, by
 // exact binade-segmented scans, ordered_sum_wave); lane 0 then updates h_hat.
-// y is read from HBM once; LDS per codeword is 16 S + 2 S bytes (+ 1 KB), so
-// 7 codewords share a CU for QPSK/PEG2304.
+// y is read from HBM once; LDS per codeword is 16 S + S bytes + 12 per word
+// (km_lds), so 8 codewords share a CU for QPSK/PEG2304 (7 with the full-length
+// member list: 3.65 -> see DESIGN.md).
 //
 // Per-iteration latency is what bounds this kernel (each codeword is a chain
 // of dependent steps; a dependent VALU step costs ~40 cycles with 3-4 waves
@@ -288,6 +289,23 @@ __global__ void km_final_kernel(const double *__restrict__ cons, const double *_
 // iterations each): 4.28 ms -> 3.31 ms; tools/km_stamps.py gives the phases.
 constexpr int kFusedT = 128;  // two waves per codeword (the two sum chains), up to 7 codewords per CU (LDS)
 constexpr int kFusedMaxW = 64;  // 64-symbol words: S <= 4096
+// Dynamic LDS of one codeword: the symbols [S] double2, the compacted member
+// list [cap + 24] u16 (cap = S/2 rounded up to 8: cluster 0 of a constellation
+// of >= 2 points; a larger cluster, seen only on degenerate inputs, is summed
+// straight from the membership words), the membership words [Sw] u64 and their
+// drift thresholds [Sw] float.  PEG2304/QPSK: 20,272 bytes + ~120 static, so 8
+// codewords share a CU (the 16 KB register budget of 4 waves per SIMD allows 8).
+struct KmLds {
+  int cap, off_mem, off_wbits, off_wthr, bytes;
+};
+__host__ __device__ constexpr KmLds km_lds(int S) {
+  const int cap = ((S + 1) / 2 + 7) & ~7;
+  const int Sw = (S + 63) / 64;
+  const int off_mem = 16 * S;
+  const int off_wbits = (off_mem + 2 * (cap + 24) + 7) & ~7;
+  const int off_wthr = off_wbits + 8 * Sw;
+  return KmLds{cap, off_mem, off_wbits, off_wthr, off_wthr + 4 * Sw};
+}
 
 // Phase timing (stamps build, -DKML_STAMPS=1; tools/km_stamps.py): thread 0's
 // s_memtime deltas summed over workgroups, plus event counts.
@@ -695,12 +713,13 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
                                                            double2 *__restrict__ h_hat, double2 *__restrict__ h4,
                                                            double2 *__restrict__ hat_out, int incremental, int scan) {
   extern __shared__ __attribute__((aligned(16))) unsigned char kmem[];
+  const KmLds L = km_lds(S);
   double2 *ys = reinterpret_cast<double2 *>(kmem);  // [S] symbols
-  // compacted cluster-0 member indices, ascending: [S + 24], 16-byte aligned
-  unsigned short *mem = reinterpret_cast<unsigned short *>(ys + S);
+  // compacted cluster-0 member indices, ascending: [cap + 24], 16-byte aligned
+  unsigned short *mem = reinterpret_cast<unsigned short *>(kmem + L.off_mem);
+  uint64_t *wbits = reinterpret_cast<uint64_t *>(kmem + L.off_wbits);  // [Sw] membership words
+  float *wthr = reinterpret_cast<float *>(kmem + L.off_wthr);  // per word: min over its symbols of D(ref) + g / (2 Cmax)
   __shared__ double2 cl[KC];
-  __shared__ uint64_t wbits[kFusedMaxW];
-  __shared__ float wthr[kFusedMaxW];  // per word: min over its symbols of D(ref) + g / (2 Cmax)
   __shared__ double red_d[kFusedT / 64];
   __shared__ int red_i[kFusedT / 64];
   __shared__ double2 s_hat;
@@ -788,7 +807,7 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
   cplx prevk{0.0, 0.0};
   cplx hprev = hat;
   double drift = 0.0;  // D: the same value in every thread
-  if (tid < kFusedMaxW) wthr[tid] = -1.0f;  // every word is assigned in the first iteration
+  if (tid < Sw) wthr[tid] = -1.0f;  // every word is assigned in the first iteration
   double sr = 0.0, si = 0.0;  // cumulative cluster-0 sum (kmeans.cc:33-34, 46)
   int cnt = 0;
   int nmem = 0;  // members in the current list
@@ -899,7 +918,7 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
                               (unsigned)__builtin_amdgcn_readlane((int)bl, w);
         if ((bits >> lane) & 1) {
           const int p = __builtin_amdgcn_readlane(excl, w) + __popcll(bits & ((1ull << lane) - 1));
-          mem[p] = (unsigned short)(w * 64 + lane);
+          if (p < L.cap) mem[p] = (unsigned short)(w * 64 + lane);
         }
       }
       __syncthreads();
@@ -907,7 +926,17 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
     KM_STAMP(KS_COMPACT);
     const int n = nmem;
     cnt += n;
-    if (scan) {  // wave 0: the real chain, wave 1: the imaginary chain (kFusedT = 128)
+    if (n > L.cap) {  // more members than the list holds (degenerate input): straight from the words
+      if (tid < 2) {  // lane 0: real chain, lane 1: imaginary chain, ascending j
+        double acc = tid == 0 ? sr : si;
+        const double *yv = reinterpret_cast<const double *>(ys) + tid;
+        for (int w = 0; w < Sw; ++w)
+          for (uint64_t b = wbits[w]; b; b &= b - 1) acc = acc + yv[2 * (w * 64 + __builtin_ctzll(b))];
+        const double other = __shfl_xor(acc, 1);
+        sr = tid == 0 ? acc : other;
+        si = tid == 0 ? other : acc;
+      }
+    } else if (scan) {  // wave 0: the real chain, wave 1: the imaginary chain (kFusedT = 128)
       int steps = 0;
       const double acc = ordered_sum_wave(wave == 0 ? sr : si, reinterpret_cast<const double *>(ys) + wave, mem, n, S,
                                           lane, steps);
@@ -955,7 +984,7 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
 template <int KC>
 bool run_kmeans_fused(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
                       double2 *h_hat, double2 *h4, double2 *hat_out, hipStream_t s, hipError_t &err) {
-  const size_t lds = sizeof(double2) * (size_t)S + 2 * (size_t)((S + 24 + 7) & ~7);
+  const size_t lds = (size_t)km_lds(S).bytes;
   if (S > 64 * kFusedMaxW || lds > 128 * 1024) return false;
   if (const char *e = getenv("KML_KMEANS"))
     if (e[0] == 's') return false;  // KML_KMEANS=split: the two-launch form (A/B)
