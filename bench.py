@@ -55,8 +55,9 @@ KERNEL_NOTES = {
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 dense peak (vector = matrix rate, AMD spec)
 # sources whose code the PMC summary describes (profiles/pmc_bp.json src_sha)
-PMC_SOURCES = ["bp_regular.hip", "bp_common.hpp", "demap_common.hpp", "exact_math.hpp", "kernels.hpp",
-               "layout.cpp", "capi.cpp"]
+# every kernel and launcher source: a PMC map entry is current only at the sources it was taken at
+PMC_SOURCES = sorted(f for f in os.listdir(os.path.join(REPO, "kmldpc_amd", "csrc"))
+                     if f.endswith((".hip", ".hpp", ".cpp")))
 
 
 def src_sha():
