@@ -85,7 +85,8 @@ template <int MB, bool EXACT>
 __device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const double2 *__restrict__ y, int S,
                                                const double2 *__restrict__ h4, int nc, double var, double inv_var,
                                                double *__restrict__ metrics, int32_t *__restrict__ chosen,
-                                               unsigned char *smem, lds_cons cl, lds_exptab etab) {
+                                               unsigned char *smem, lds_cons cl, lds_exptab etab, lds_cons scr,
+                                               double scb) {
   int *cnt = reinterpret_cast<int *>(smem);  // 4 counters, the undecided flag, the unproven flag
   unsigned char *hb = smem + 32;             // [4][cc_len]
   constexpr bool kRescan = MB >= 5;
@@ -98,7 +99,7 @@ __device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const d
     const double2 v = yy[j];
     const double2 hh = h4[(long long)cw * nc + q];
     unsigned bits;
-    if (!hard_bits_screen<MB>(cl, v.x, v.y, hh.x, hh.y, inv_var, bits)) {
+    if (!hard_bits_screen<MB>(scr, scb, v.x, v.y, hh.x, hh.y, inv_var, bits)) {
       if (kRescan) {
         hb[q * c.cc_len + j * MB] = 2;  // undecided: the demap pass below
         cnt[4] = 1;
@@ -175,6 +176,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? 3
     int nc, double var, double inv_var, double *__restrict__ metrics, int32_t *__restrict__ chosen, DemapDefer d) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ double cl[2 << MB];
+  __shared__ double scr[3 << MB];  // the screen's (|c_k|^2, 2 Re c_k, 2 Im c_k)
+  __shared__ double scb;           // the screen's bound on the constellation (hard_bits_screen)
   __shared__ uint64_t etab[256];
   unsigned todo = 1;
   if constexpr (EXACT) {
@@ -182,16 +185,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? 3
     if (blockIdx.x >= todo) return;
   }
   for (int k = threadIdx.x; k < (2 << MB); k += blockDim.x) cl[k] = cons[k];
+  for (int k = threadIdx.x; k < (1 << MB); k += blockDim.x) {
+    const double cr = cons[2 * k], ci = cons[2 * k + 1];
+    scr[3 * k] = cr * cr + ci * ci;
+    scr[3 * k + 1] = 2.0 * cr;
+    scr[3 * k + 2] = 2.0 * ci;
+  }
+  if (threadIdx.x == 0) {  // max(max |c|^2, 2 max(|Re c|, |Im c|)), rounded up
+    double b = 0.0;
+    for (int k = 0; k < (1 << MB); ++k) {
+      const double cr = cons[2 * k], ci = cons[2 * k + 1];
+      b = fmax(b, fmax(cr * cr + ci * ci, 2.0 * fmax(fabs(cr), fabs(ci))));
+    }
+    scb = b * (1.0 + 0x1p-40);
+  }
   stage_exp_table(etab);
   __syncthreads();
   if constexpr (EXACT) {
     for (unsigned i = blockIdx.x; i < todo; i += gridDim.x)
       cand_metric_cw<MB, true>(d.idx[i], c, y, S, h4, nc, var, inv_var, metrics, chosen, smem, (lds_cons)cl,
-                               (lds_exptab)etab);
+                               (lds_exptab)etab, (lds_cons)scr, scb);
   } else {
     const int cw = blockIdx.x;
     if (!cand_metric_cw<MB, false>(cw, c, y, S, h4, nc, var, inv_var, metrics, chosen, smem, (lds_cons)cl,
-                                   (lds_exptab)etab) &&
+                                   (lds_exptab)etab, (lds_cons)scr, scb) &&
         threadIdx.x == 0)
       d.idx[atomicAdd(d.cnt, 1u)] = cw;
   }

@@ -193,18 +193,26 @@ __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double 
 // 1e-12.  Each c_k is then within 1e-5 relative of the reference's, the
 // sums q within 1.5e-5, and the reference's own rounding is below 1e-13: a bit
 // is decided only when one sum exceeds the other by 2^-12 (2.4e-4) relative.
+// The distances enter only through a_k = dmin - d_k, so the common |y|^2 / var
+// drops out: d_k - |y|^2/var = |c_k|^2 A - 2 Re(c_k B) with A = |h|^2 / var and
+// B = h conj(y) / var, three fp64 operations per point from the staged
+// (|c_k|^2, 2 Re c_k, 2 Im c_k) (scr; the reference's form costs nine).  Their
+// rounding errors are below 2^-50 M, M = max_k (|c_k|^2 |A| + 2 |c_k| |B|) <=
+// 2^20 (checked; beyond it the symbol takes the exact path), i.e. under 1e-9
+// absolute in a_k: far inside the float rounding of a_k the margin covers.
 template <int MB, class CP>
-__device__ __forceinline__ bool hard_bits_screen(CP cons, double yr, double yi, double hr,
+__device__ __forceinline__ bool hard_bits_screen(CP scr, double cbound, double yr, double yi, double hr,
                                                  double hi, double inv_var, unsigned &bits) {
   constexpr int KC = 1 << MB;
+  asm volatile("" : "+v"(scr));  // opaque per call: no hoisting of the point loads out of the caller's loop
+  const double A = (hr * hr + hi * hi) * inv_var;
+  const double Br = (hr * yr + hi * yi) * inv_var;  // Re(h conj(y)) / var
+  const double Bi = (hi * yr - hr * yi) * inv_var;  // Im(h conj(y)) / var
+  // cbound = (max |c_k|^2, max(|Re c_k|, |Im c_k|)) folded: M <= cb2 A + 2 cab (|Br| + |Bi|)
+  if (!(cbound * (A + fabs(Br) + fabs(Bi)) <= 0x1p20)) return false;
+  auto dist = [&](int k) { return fma(scr[3 * k], A, -fma(scr[3 * k + 1], Br, -(scr[3 * k + 2] * Bi))); };
   // for large constellations d_k is computed twice (for dmin, then for a_k)
   // rather than kept: KC doubles would cost 2 KC registers
-  auto dist = [&](int k) {
-    const double cr = cons[2 * k], ci = cons[2 * k + 1];
-    const double sr = cr * hr - ci * hi - yr;
-    const double si = cr * hi + ci * hr - yi;
-    return (sr * sr + si * si) * inv_var;
-  };
   constexpr bool kRecompute = KC >= 32;
   double dk[kRecompute ? 1 : KC];
   double dmin = 0.0;
@@ -214,7 +222,7 @@ __device__ __forceinline__ bool hard_bits_screen(CP cons, double yr, double yi, 
     if (!kRecompute) dk[k] = d;
     dmin = k == 0 ? d : fmin(dmin, d);
   }
-  if (kRecompute) asm volatile("" : "+v"(cons));  // reload the points (no CSE across the passes)
+  if (kRecompute) asm volatile("" : "+v"(scr));  // reload the points (no CSE across the passes)
   float e[KC];
   float sum = 0.f;
 #pragma unroll
