@@ -99,7 +99,7 @@ __device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const d
     const double2 v = yy[j];
     const double2 hh = h4[(long long)cw * nc + q];
     unsigned bits;
-    if (!hard_bits_screen<MB>(scr, scb, v.x, v.y, hh.x, hh.y, inv_var, bits)) {
+    if (!hard_bits_screen<MB>(cl, scr, scb, v.x, v.y, hh.x, hh.y, inv_var, bits)) {
       if (kRescan) {
         hb[q * c.cc_len + j * MB] = 2;  // undecided: the demap pass below
         cnt[4] = 1;

@@ -719,10 +719,9 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
   unsigned short *mem = reinterpret_cast<unsigned short *>(kmem + L.off_mem);
   uint64_t *wbits = reinterpret_cast<uint64_t *>(kmem + L.off_wbits);  // [Sw] membership words
   float *wthr = reinterpret_cast<float *>(kmem + L.off_wthr);  // per word: min over its symbols of D(ref) + g / (2 Cmax)
-  __shared__ double2 cl[KC];
+  __shared__ double2 clw[kFusedT / 64][KC];  // each wave's own copy of the clusters (no barrier)
   __shared__ double red_d[kFusedT / 64];
   __shared__ int red_i[kFusedT / 64];
-  __shared__ double2 s_hat;
   __shared__ int s_exact;
   __shared__ int s_flag[1 + kFusedT / 64];  // converged; per wave: member bits changed
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -737,6 +736,9 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
   const double2 *yy = y + (long long)cw * S;
   for (int j = tid; j < S; j += kFusedT) ys[j] = yy[j];
   if (tid == 0) s_exact = 0;
+  // every word is assigned in the first iteration (set before the prologue's
+  // barriers: the iterations have none before their first assignment)
+  if (tid < Sw) wthr[tid] = -1.0f;
   __syncthreads();
 
   // ---- first max |y| (kmeans.cc:17-22), screened like first_max_abs
@@ -807,7 +809,6 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
   cplx prevk{0.0, 0.0};
   cplx hprev = hat;
   double drift = 0.0;  // D: the same value in every thread
-  if (tid < Sw) wthr[tid] = -1.0f;  // every word is assigned in the first iteration
   double sr = 0.0, si = 0.0;  // cumulative cluster-0 sum (kmeans.cc:33-34, 46)
   int cnt = 0;
   int nmem = 0;  // members in the current list
@@ -815,7 +816,11 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
   for (int it = 0; it < iters; ++it) {
     // clusters_[k] = c[k] * hatH, and the convergence test against
     // tempClusters (kmeans.cc:26-28 / 72-74, 47-56)
-    if (wave == 0) {  // KC <= 64: one wave computes the clusters and the test
+    // Both waves compute the clusters and the test (KC <= 64: lanes k < KC) on
+    // the same hatH, into their own copies: the same values, no barrier.
+    double2 *cl = clw[wave];
+    int conv;
+    {
       bool same = true;
       if (lane < KC) {
         const cplx p = kml_cmul(cplx{cons[2 * lane], cons[2 * lane + 1]}, hat);
@@ -823,11 +828,9 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
         same = (p.re == prevk.re) && (p.im == prevk.im);
         prevk = p;
       }
-      const bool all = __ballot(!same) == 0;
-      if (lane == 0) s_flag[0] = all;
+      conv = __ballot(!same) == 0;
+      __builtin_amdgcn_wave_barrier();  // the wave's cluster stores precede its loads below (LDS in order per wave)
     }
-    __syncthreads();
-    const int conv = s_flag[0];
     KM_STAMP(KS_CLUSTERS);
     if (conv) break;  // the reference breaks after an assignment it then discards
     KM_COUNT(KS_ITERS, 1);
@@ -932,37 +935,29 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
         const double *yv = reinterpret_cast<const double *>(ys) + tid;
         for (int w = 0; w < Sw; ++w)
           for (uint64_t b = wbits[w]; b; b &= b - 1) acc = acc + yv[2 * (w * 64 + __builtin_ctzll(b))];
-        const double other = __shfl_xor(acc, 1);
-        sr = tid == 0 ? acc : other;
-        si = tid == 0 ? other : acc;
+        red_d[tid] = acc;
       }
     } else if (scan) {  // wave 0: the real chain, wave 1: the imaginary chain (kFusedT = 128)
       int steps = 0;
       const double acc = ordered_sum_wave(wave == 0 ? sr : si, reinterpret_cast<const double *>(ys) + wave, mem, n, S,
                                           lane, steps);
       KM_COUNT(KS_STEPS, steps);
-      if (wave == 0) sr = acc;
-      if (wave == 1) {
-        si = acc;
-        if (lane == 0) red_d[0] = acc;
-      }
-      __syncthreads();
-      if (tid == 0) si = red_d[0];
+      if (lane == 0) red_d[wave] = acc;
     } else if (tid < 2) {  // lane 0: real chain, lane 1: imaginary chain, ascending j
-      const double acc = ordered_sum(tid == 0 ? sr : si, reinterpret_cast<const double *>(ys) + tid, mem, n, S);
-      const double other = __shfl_xor(acc, 1);
-      sr = tid == 0 ? acc : other;
-      si = tid == 0 ? other : acc;
-    }
-    KM_STAMP(KS_SUM);
-    if (tid == 0) {
-      const cplx m0 = cdiv_count(sr, si, cnt);  // kmeans.cc:59-62
-      const cplx nh = cdiv_const(m0, c0, c0k);  // kmeans.cc:64-71
-      s_hat = make_double2(nh.re, nh.im);
+      red_d[tid] = ordered_sum(tid == 0 ? sr : si, reinterpret_cast<const double *>(ys) + tid, mem, n, S);
     }
     __syncthreads();
+    sr = red_d[0];
+    si = red_d[1];
+    KM_STAMP(KS_SUM);
+    // every lane of both waves updates hatH (the same operations on the same
+    // values, kmeans.cc:59-71): no broadcast, no barrier
+    {
+      const cplx m0 = cdiv_count(sr, si, cnt);  // kmeans.cc:59-62
+      const cplx nh = cdiv_const(m0, c0, c0k);  // kmeans.cc:64-71
+      hat = nh;
+    }
     KM_STAMP(KS_UPDATE);
-    hat = cplx{s_hat.x, s_hat.y};
   }
 #if KML_STAMPS
   if (tid == 0) {
