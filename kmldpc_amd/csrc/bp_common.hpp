@@ -174,7 +174,7 @@ __device__ __forceinline__ void cn_norm_rows(const double (&n0)[R], const double
 // Diagnostic build (-DKML_DIV_STATS=1, `make variant`): counts of the FAST
 // VN divisions' failed premises and checks per translation unit, and the
 // operands of the first 64 failures ([0] pairs seen (per wave), [1] !ok,
-// [2] q0 unproven, [3] q1 unproven, [4] max |e1| bits, [8 + 5 i ..] samples:
+// [2] q0 unproven, [3] q1 unproven, [4] max |e0| bits (v_rcp_f64), [8 + 5 i ..] samples:
 // n0, n1, s, q0, q1).  Read by kml_debug_div_stats.
 #ifndef KML_DIV_STATS
 #define KML_DIV_STATS 0

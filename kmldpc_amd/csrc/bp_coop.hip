@@ -1175,10 +1175,17 @@ __device__ __forceinline__ int part_iterations_tagged(
             const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
             const double q = clip_c2v<true>(div1<true, true>(t0, t0 + t1));
             if (cact[r]) {
-              const int e = odd ? st : DC - 1 - st;  // the edge this c2v belongs to
-              const int mask = crx[r] & 0xFF;
+              // the store's addresses are recomputed here from opaque copies
+              // of crx and odd: hoisted out of the iteration loop, the 2 x 3
+              // per-lane mailbox offsets, masks and LDS addresses were spilled,
+              // and each c2v store waited on a scratch reload (s_waitcnt
+              // vmcnt(0) behind every outstanding store)
+              int cr = crx[r], od = odd;
+              asm volatile("" : "+v"(cr), "+v"(od));
+              const int e = od ? st : DC - 1 - st;  // the edge this c2v belongs to
+              const int mask = cr & 0xFF;
               if ((mask >> e) & 1) {
-                const int x = (crx[r] >> 8) + __popc(mask & ((1 << e) - 1));
+                const int x = (cr >> 8) + __popc(mask & ((1 << e) - 1));
                 mb_st64(tb, tb_c2v + (unsigned)x * 8, or_hi(q, tag ? kTagHi : 0u));
               } else {
                 *reinterpret_cast<double *>(smem + cbase[r] + e * 16) = q;

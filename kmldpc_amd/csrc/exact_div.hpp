@@ -12,19 +12,20 @@
 // 1. dd_quot + dd_check (the decoders' FAST VN divisions, demap_common.hpp):
 //    y0 = v_rcp_f64(s), whose relative error e0 the ISA documents as at most
 //    2^29 ulp = 2^-23 (tests/test_gpu_parity.py::test_hardware_reciprocal_error
-//    measures it on the device); y1 = y0 after one Newton step, e1 = RN(1 - s y1)
-//    (fma), |e1| <= e0^2 + 2^-53 < 2^-45; ylo = RN(e1 y1).
-//    y1 + e1 y1 = (1 - e1^2) / s, so
-//        q = fma(n, y1, RN(n ylo))
-//    rounds a value within 2^-90 relative of n/s once: q is a FAITHFUL
+//    measures it on the device); e = RN(1 - s y0) (fma), ylo = RN(y0 RN(e + e^2))
+//    (one fma, one multiply: no Newton step).  With e* = 1 - s y0 exactly,
+//    y0 (1 + e* + e*^2) = (1 - e*^3) / s, and e differs from e* by at most
+//    2^-53 |e*|, so y0 + ylo = (1 + d) / s with |d| <= e0^3 + 2^-74 < 2^-68, and
+//        q = fma(n, y0, RN(n ylo))
+//    rounds a value within 2^-67 relative of n/s once: q is a FAITHFUL
 //    rounding of n/s (one of its two neighbours).  (The argument needs only
-//    |e1| <= 2^-30, i.e. e0 <= 2^-15: 2^8 below the documented bound.)
+//    e0^3 < 2^-56, i.e. e0 <= 2^-19: 2^4 below the documented bound.)
 //    The check: r = fma(-q, s, n) is exact (q faithful; n = 0 or n >= 2^-969,
-//    s and q normal), r = s (n/s - q).  With yk = RN(y1 (1 + 2^-40)),
-//        t = fma(r, yk, q) = RN(q + (n/s - q) F),  F = s yk = (1 - e1)(1 + 2^-40)(1 + eps),
-//    |eps| <= 2^-53, so 1 < F < 1 + 2^-39 whenever |e1| < 2^-40.1, i.e. e0 <=
-//    2^-20.1: 2^2.9 below the documented bound (the fma forms r yk exactly,
-//    and t rounds once).  If q != RN(n/s),
+//    s and q normal), r = s (n/s - q).  With yk = RN(y0 (1 + 2^-40) + ylo)
+//    (one fma),
+//        t = fma(r, yk, q) = RN(q + (n/s - q) F),  F = s yk = (1 + d)(1 + 2^-40) + eps',
+//    |eps'| <= 2^-52, so 1 < F < 1 + 2^-39 (the fma forms r yk exactly, and t
+//    rounds once).  If q != RN(n/s),
 //    |n/s - q| exceeds half the gap g between q and its neighbour towards n/s
 //    (g = ulp(q), or ulp(q)/2 below a power of two; n/s is never exactly a
 //    midpoint: s times a 54-bit odd significand has more than 53 bits), so
@@ -37,7 +38,9 @@
 //    with dd_fix (q faithful: RN(n/s) is q or its neighbour, told apart by
 //    their exact residuals) instead of redoing the codeword; the demapper
 //    reruns the symbol on the exact path.
-//    Cost per normalisation pair: 7 shared + 4 per quotient (+ the fix, rare).
+//    Cost per normalisation pair: v_rcp_f64 + 4 shared + 5 per quotient (+ the
+//    fix, rare).  (Round 3's first form refined y0 by a Newton step first,
+//    y1 = y0 + y0 e, e1 = 1 - s y1, ylo = e1 y1: one instruction more per pair.)
 //
 // 2. div_rn (every other division: the decoders' exact re-decode, the
 //    non-FAST demap, k-means): any operands.  Finite normal operands with
@@ -58,22 +61,21 @@
 namespace kml {
 
 struct DdRcp {
-  double hi, lo;  // y1, RN(e1 y1)
+  double hi, lo, k;  // y0, RN(y0 (e + e^2)), RN(y0 (1 + 2^-40) + lo)
 };
 
 __device__ __forceinline__ DdRcp dd_rcp(double s) {
   const double y0 = __builtin_amdgcn_rcp(s);
-  const double y1 = fma(y0, fma(-y0, s, 1.0), y0);
-  const double e1 = fma(-y1, s, 1.0);
-  return {y1, e1 * y1};
+  const double e = fma(-y0, s, 1.0);
+  const double lo = y0 * fma(e, e, e);
+  return {y0, lo, fma(y0, 1.0 + 0x1p-40, lo)};
 }
 
 __device__ __forceinline__ double dd_quot(double n, const DdRcp &y) { return fma(n, y.hi, n * y.lo); }
 
-// true when q == RN(n / s) is proven (see 1. above); the two quotients of a
-// pair share yk (common subexpression)
+// true when q == RN(n / s) is proven (see 1. above)
 __device__ __forceinline__ bool dd_check(double n, double s, double q, const DdRcp &y) {
-  return fma(fma(-q, s, n), y.hi * (1.0 + 0x1p-40), q) == q;
+  return fma(fma(-q, s, n), y.k, q) == q;
 }
 
 // RN(n / s) from a faithful q that dd_check could not prove: q or its
