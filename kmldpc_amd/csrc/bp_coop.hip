@@ -63,6 +63,22 @@ struct GroupSync {
 
 constexpr int kPartG = 4;  // workgroups per codeword of the partitioned kernel
 
+// c2v placement: a c2v message lives in the lower or upper 8 bytes of its
+// 16-byte slot (the v2c pair fills the whole slot), by bit 2 of its row's
+// member-local index for row slots and bit 2 of the slot index for mirror
+// slots.  The CN phase's 16-lane ds_write_b64 groups (8 rows, 24 dwords
+// apart) then hit distinct banks (rows q and q + 4 no longer collide), and the
+// VN phase's scattered ds_read_b64 use all 64 banks instead of the 32 of
+// slot-aligned addresses.  vaddr holds the half-slot index 2 slot + half.
+#ifndef KML_PART_C2V_HALF
+#define KML_PART_C2V_HALF 0
+#endif
+__host__ __device__ constexpr int part_c2v_half(int slot, int EG, int DC) {
+  return KML_PART_C2V_HALF ? (slot < EG ? ((slot / DC) >> 2) & 1 : (slot >> 2) & 1) : 0;
+}
+__device__ __forceinline__ unsigned vaddr_c2v(int v) { return (unsigned)(v & 0x1FFFF) * 8u; }  // c2v word (bytes)
+__device__ __forceinline__ unsigned vaddr_slot(int v) { return (unsigned)(v & 0x1FFFE) * 8u; }  // slot (bytes)
+
 // LDS of the partitioned kernel: the member's row slots, its mirror slots, and
 // every column's hard decision.
 size_t part_lds_bytes(const DevCode &c) {
@@ -622,7 +638,11 @@ __device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, 
     if (iter > 0) {  // iteration 0 reads InitMsg's 0.5
 #pragma unroll
       for (int q = 0; q < RX; ++q)
-        if (xc[q] >= 0) *reinterpret_cast<double *>(smem + (xc[q] & 0xFFFF) * 16) = ld_nt(&mb_c2v[xc[q] >> 16]);
+        if (xc[q] >= 0) {
+          const int sl = xc[q] & 0xFFFF;
+          *reinterpret_cast<double *>(smem + sl * 16 + (KML_PART_C2V_HALF ? ((sl >> 2) & 1) * 8 : 0)) =
+              ld_nt(&mb_c2v[xc[q] >> 16]);
+        }
       __syncthreads();
     }
     KML_STAMP(1);  // receive c2v
@@ -633,7 +653,7 @@ __device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, 
 #pragma unroll
       for (int r = 0; r < RV; ++r)
 #pragma unroll
-        for (int k = 0; k < DV; ++k) c0s[r][k] = *reinterpret_cast<const double *>(smem + (vaddr[r][k] & 0xFFFF) * 16);
+        for (int k = 0; k < DV; ++k) c0s[r][k] = *reinterpret_cast<const double *>(smem + vaddr_c2v(vaddr[r][k]));
       // one column's chains at a time (column-major): the FAST divisions'
       // proofs keep a normalisation's operands live, and interleaving the RV
       // columns step by step doubled the live set (scratch spills in the loop)
@@ -669,7 +689,7 @@ __device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, 
             div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
           else
             div2<FAST>(t0, t1, t0 + t1, q0, q1, sus);
-          if (vact[r]) *reinterpret_cast<double2 *>(smem + (vaddr[r][k] & 0xFFFF) * 16) = make_double2(q0, q1);
+          if (vact[r]) *reinterpret_cast<double2 *>(smem + vaddr_slot(vaddr[r][k])) = make_double2(q0, q1);
           if (k > 0) {
             const double c0 = c0s[r][k];
             if (unit) {  // the sum rounds to exactly 1 (bp_common.hpp)
@@ -760,7 +780,9 @@ __device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, 
             const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
             const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
             const double q = clip_c2v<FAST>(div1<FAST, true>(t0, t0 + t1));
-            if (cact[r]) *reinterpret_cast<double *>(smem + cbase[r] + (odd ? st : DC - 1 - st) * 16) = q;
+            if (cact[r])
+              *reinterpret_cast<double *>(smem + cbase[r] + (odd ? st : DC - 1 - st) * 16 +
+                                          part_c2v_half(cbase[r] / 16, 0x7FFFFFFF, DC) * 8) = q;
           }
         }
         if (advance) {
@@ -851,6 +873,7 @@ __device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, 
 constexpr unsigned kTagHi = 0x80000000u;  // bit 63 of a message word (hi dword bit 31)
 constexpr unsigned kHdHi = 0x40000000u;   // bit 62: hard decision (v2c first word)
 
+
 __device__ __forceinline__ double or_hi(double x, unsigned bits) {
   return __hiloint2double(__double2hiint(x) | (int)bits, __double2loint(x));
 }
@@ -927,7 +950,9 @@ __device__ __forceinline__ bool poll_entries(const int (&ent)[R], __amdgpu_buffe
         for (int i = 0; i < W; ++i) ok = ok && (hi_of(w[q][i]) >> 31) == tag;
         if (ok) {
           // stored without the tags (a v2c message keeps its hard-decision bit)
-          unsigned long long *d = reinterpret_cast<unsigned long long *>(smem + (ent[q] & 0xFFFF) * 16);
+          const int sl = ent[q] & 0xFFFF;
+          unsigned long long *d = reinterpret_cast<unsigned long long *>(
+              smem + sl * 16 + (W == 1 && KML_PART_C2V_HALF ? ((sl >> 2) & 1) * 8 : 0));
 #pragma unroll
           for (int i = 0; i < W; ++i) d[i] = w[q][i] & ~(1ull << 63);
           need[q] = false;
@@ -1003,7 +1028,7 @@ __device__ __forceinline__ int part_iterations_tagged(
       for (int r = 0; r < RV; ++r) {
         double c0c[DV];  // the column's c2v, loaded per column (registers)
 #pragma unroll
-        for (int k = 0; k < DV; ++k) c0c[k] = *reinterpret_cast<const double *>(smem + (vaddr[r][k] & 0xFFFF) * 16);
+        for (int k = 0; k < DV; ++k) c0c[k] = *reinterpret_cast<const double *>(smem + vaddr_c2v(vaddr[r][k]));
         double a0 = pv[r], a1 = 1.0 - pv[r], al0[DV], al1[DV];
         unsigned hdb = 0;
 #pragma unroll
@@ -1034,12 +1059,12 @@ __device__ __forceinline__ int part_iterations_tagged(
           else
             div2<true>(t0, t1, t0 + t1, q0, q1, sus);
           if (vact[r]) {
-            const int x1 = vaddr[r][k] >> 16;  // mailbox index + 1 of a cut edge, 0 for a row slot
+            const int x1 = (int)((unsigned)vaddr[r][k] >> 17);  // mailbox index + 1 of a cut edge, 0 for a row slot
             if (x1) {
               const unsigned tb_tag = tag ? kTagHi : 0u;
               mb_st128(tb, (unsigned)(x1 - 1) * 16, or_hi(q0, tb_tag | hdb), or_hi(q1, tb_tag));
             } else {
-              *reinterpret_cast<double2 *>(smem + (vaddr[r][k] & 0xFFFF) * 16) = make_double2(or_hi(q0, hdb), q1);
+              *reinterpret_cast<double2 *>(smem + vaddr_slot(vaddr[r][k])) = make_double2(or_hi(q0, hdb), q1);
             }
           }
           if (k > 0) {
@@ -1092,7 +1117,7 @@ __device__ __forceinline__ int part_iterations_tagged(
 #pragma unroll
         for (int r = 0; r < RC; ++r)
           if (cact[r]) {
-            const int mask = crx[r] & 0xFF;
+            const int mask = crx[r] & 0x3F;
 #pragma unroll
             for (int k = 0; k < H; ++k) {
               const int e = odd ? H + k : k;
@@ -1183,12 +1208,12 @@ __device__ __forceinline__ int part_iterations_tagged(
               int cr = crx[r], od = odd;
               asm volatile("" : "+v"(cr), "+v"(od));
               const int e = od ? st : DC - 1 - st;  // the edge this c2v belongs to
-              const int mask = cr & 0xFF;
+              const int mask = cr & 0x3F;  // bit 7: the row's c2v half (kernel setup)
               if ((mask >> e) & 1) {
                 const int x = (cr >> 8) + __popc(mask & ((1 << e) - 1));
                 mb_st64(tb, tb_c2v + (unsigned)x * 8, or_hi(q, tag ? kTagHi : 0u));
               } else {
-                *reinterpret_cast<double *>(smem + cbase[r] + e * 16) = q;
+                *reinterpret_cast<double *>(smem + cbase[r] + e * 16 + ((cr >> 4) & 8)) = q;
               }
             }
           }
@@ -1269,7 +1294,7 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
   const int nslots = EG + c.pt_mirror;
   uint8_t *dec = smem + (size_t)nslots * 16;  // N hard decisions, plan order
 
-  // vaddr: (mailbox index + 1 of a cut edge, 0 for a row slot) << 16 | LDS slot (row slot or mirror)
+  // vaddr: (mailbox index + 1 of a cut edge, 0 for a row slot) << 17 | (2 LDS slot + c2v half)
   int vaddr[RV][DV], vpos[RV];
   bool vact[RV];
 #pragma unroll
@@ -1279,7 +1304,10 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     vpos[r] = member * NG + (vact[r] ? i : 0);
 #pragma unroll
     for (int k = 0; k < DV; ++k)
-      vaddr[r][k] = ((c.pt_vx[vpos[r] * DV + k] + 1) << 16) | (c.pt_vaddr[vpos[r] * DV + k] >> 4);
+    {
+      const int sl = c.pt_vaddr[vpos[r] * DV + k] >> 4;
+      vaddr[r][k] = ((c.pt_vx[vpos[r] * DV + k] + 1) << 17) | (2 * sl + part_c2v_half(sl, EG, DC));
+    }
   }
   int crow[RC], cbase[RC], crx[RC];
   bool cact[RC];
@@ -1291,7 +1319,7 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     const int row = c.pt_cn[member * MG + li];
     crow[r] = row;
     cbase[r] = li * DC * 16;
-    crx[r] = c.pt_rx[member * MG + li];
+    crx[r] = c.pt_rx[member * MG + li] | (part_c2v_half(li * DC, EG, DC) << 7);
   }
   int xr[RX], xc[RX];
   {

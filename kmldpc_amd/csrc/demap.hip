@@ -32,8 +32,14 @@ namespace {
 // defer list (d.idx, up to d.cap entries; the count runs on past the cap).
 // EXACT: the listed symbols on the exact path (div_rn, kml_exp), or, when the
 // list overflowed, every symbol carrying the sentinel.
+// 64QAM: the 64 probabilities of a symbol stay in registers (280 VGPRs
+// unconstrained, one wave per SIMD); KML_DEMAP64_WAVES = 2 caps the kernel at
+// 256 so two waves per SIMD hide the exp table loads and the dependent chains
+#ifndef KML_DEMAP64_WAVES
+#define KML_DEMAP64_WAVES 2
+#endif
 template <int MB, bool EXACT>
-__global__ __launch_bounds__(256) void demap_kernel(const double *__restrict__ cons, const double2 *__restrict__ y,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? KML_DEMAP64_WAVES : 1))) void demap_kernel(const double *__restrict__ cons, const double2 *__restrict__ y,
                                                     int S, int reps, const double2 *__restrict__ h, int h_stride,
                                                     const int32_t *__restrict__ h_sel, double var, int B,
                                                     double *__restrict__ p0, DemapDefer d) {

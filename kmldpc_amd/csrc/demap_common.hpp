@@ -250,16 +250,31 @@ __device__ __forceinline__ bool hard_bits_screen(CP cons, CP scr, double cbound,
   float q0[MB], q1[MB];
 #pragma unroll
   for (int j = 0; j < MB; ++j) q0[j] = q1[j] = 0.f;
+  // 16QAM and up: q1_j = total - q0_j (half the label-sum adds).  Its error
+  // is at most 2^-24 (KC + 1) total beside q0_j's; a wrong call needs the true
+  // sums ordered the other way, where the smaller-labelled sum is at least
+  // total / 2, so the extra error stays below 2^-17 relative to the sums
+  // compared, far inside the 2^-12 margin.
+#ifndef KML_SCREEN_COMPLEMENT
+#define KML_SCREEN_COMPLEMENT 0
+#endif
+  constexpr bool kComplement = KML_SCREEN_COMPLEMENT && MB >= 4;
+  float tot = 0.f;
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
     const float c = fminf(fmaxf(e[k] * inv, 1e-12f), 1.f);
+    if (kComplement) tot += c;
 #pragma unroll
     for (int j = 0; j < MB; ++j) {
       if (((k >> (MB - 1 - j)) & 1) == 0)
         q0[j] += c;
-      else
+      else if (!kComplement)
         q1[j] += c;
     }
+  }
+  if (kComplement) {
+#pragma unroll
+    for (int j = 0; j < MB; ++j) q1[j] = tot - q0[j];
   }
   constexpr float g = 1.f + 0x1p-12f;
   unsigned b = 0;
