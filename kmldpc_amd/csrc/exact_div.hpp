@@ -64,11 +64,20 @@ struct DdRcp {
   double hi, lo, k;  // y0, RN(y0 (e + e^2)), RN(y0 (1 + 2^-40) + lo)
 };
 
+#ifndef KML_DD_NEWTON
+#define KML_DD_NEWTON 0
+#endif
 __device__ __forceinline__ DdRcp dd_rcp(double s) {
   const double y0 = __builtin_amdgcn_rcp(s);
+#if KML_DD_NEWTON  // (A/B) round 3's first form: one Newton step, y1 + RN(e1 y1), yk = RN(y1 (1 + 2^-40))
+  const double y1 = fma(y0, fma(-y0, s, 1.0), y0);
+  const double e1 = fma(-y1, s, 1.0);
+  return {y1, e1 * y1, y1 * (1.0 + 0x1p-40)};
+#else
   const double e = fma(-y0, s, 1.0);
   const double lo = y0 * fma(e, e, e);
   return {y0, lo, fma(y0, 1.0 + 0x1p-40, lo)};
+#endif
 }
 
 __device__ __forceinline__ double dd_quot(double n, const DdRcp &y) { return fma(n, y.hi, n * y.lo); }
