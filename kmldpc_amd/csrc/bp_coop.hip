@@ -71,7 +71,7 @@ constexpr int kPartG = 4;  // workgroups per codeword of the partitioned kernel
 // VN phase's scattered ds_read_b64 use all 64 banks instead of the 32 of
 // slot-aligned addresses.  vaddr holds the half-slot index 2 slot + half.
 #ifndef KML_PART_C2V_HALF
-#define KML_PART_C2V_HALF 0
+#define KML_PART_C2V_HALF 1
 #endif
 __host__ __device__ constexpr int part_c2v_half(int slot, int EG, int DC) {
   return KML_PART_C2V_HALF ? (slot < EG ? ((slot / DC) >> 2) & 1 : (slot >> 2) & 1) : 0;

@@ -256,7 +256,7 @@ __device__ __forceinline__ bool hard_bits_screen(CP cons, CP scr, double cbound,
   // total / 2, so the extra error stays below 2^-17 relative to the sums
   // compared, far inside the 2^-12 margin.
 #ifndef KML_SCREEN_COMPLEMENT
-#define KML_SCREEN_COMPLEMENT 0
+#define KML_SCREEN_COMPLEMENT 1
 #endif
   constexpr bool kComplement = KML_SCREEN_COMPLEMENT && MB >= 4;
   float tot = 0.f;

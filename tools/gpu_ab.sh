@@ -11,7 +11,7 @@ if [ "${TESTS:-0}" = 1 ]; then
   rc=$?; echo "tests rc=$rc" >> $O/summary.txt
   [ $rc = 0 ] || [ $rc = 1 ] || exit $rc   # 1 = failed tests: benches still run; anything else stops the GPU
 fi
-for r in 1 2; do
+for r in $(seq 1 ${ROUNDS:-2}); do
   for w in ${WORKLOADS:-headline}; do
     E=""
     case $w in
