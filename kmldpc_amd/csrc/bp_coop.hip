@@ -804,7 +804,10 @@ __device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, 
     KML_STAMP(7);  // CN drain (other waves)
 #pragma unroll
     for (int q = 0; q < RX; ++q)
-      if (xr[q] >= 0) mb_c2v[xr[q] >> 16] = slots[xr[q] & 0xFFFF].x;
+      if (xr[q] >= 0) {  // the row slot's c2v half (part_c2v_half)
+        const int sl = xr[q] & 0xFFFF;
+        mb_c2v[xr[q] >> 16] = part_c2v_half(sl, 0x7FFFFFFF, DC) ? slots[sl].y : slots[sl].x;
+      }
     const int failing = part_barrier<kG>(gs, bst, nb, same_xcd, abort, sfail);
     KML_STAMP(8);  // send c2v + group barrier
     if (failing < 0) return -1;
