@@ -12,17 +12,22 @@
 // 1. dd_quot + dd_check (the decoders' FAST VN divisions, demap_common.hpp):
 //    y0 = v_rcp_f64(s), whose relative error e0 the ISA documents as at most
 //    2^29 ulp = 2^-23 (tests/test_gpu_parity.py::test_hardware_reciprocal_error
-//    measures it on the device); e = RN(1 - s y0) (fma), ylo = RN(y0 RN(e + e^2))
-//    (one fma, one multiply: no Newton step).  With e* = 1 - s y0 exactly,
-//    y0 (1 + e* + e*^2) = (1 - e*^3) / s, and e differs from e* by at most
-//    2^-53 |e*|, so y0 + ylo = (1 + d) / s with |d| <= e0^3 + 2^-74 < 2^-68, and
-//        q = fma(n, y0, RN(n ylo))
-//    rounds a value within 2^-67 relative of n/s once: q is a FAITHFUL
+//    measures it on the device).  Shipped form (KML_DD_NEWTON = 1): one Newton
+//    step y1 = y0 + y0 RN(1 - s y0), e1 = RN(1 - s y1) (fma), |e1| <= e0^2 +
+//    2^-53 < 2^-45, hi = y1, ylo = RN(e1 y1), yk = RN(y1 (1 + 2^-40)).
+//    y1 + e1 y1 = (1 - e1^2) / s.  Alternative (KML_DD_NEWTON = 0, one
+//    instruction less per pair but measured 2.7 % slower on the headline BP
+//    kernel: its yk waits on ylo): hi = y0, e = RN(1 - s y0),
+//    ylo = RN(y0 RN(e + e^2)), yk = RN(y0 (1 + 2^-40) + ylo); y0 (1 + e* + e*^2)
+//    = (1 - e*^3) / s.  Either way y0 + ylo (resp. y1 + ylo) is within 2^-67 of
+//    1/s, and
+//        q = fma(n, hi, RN(n ylo))
+//    rounds a value within 2^-66 relative of n/s once: q is a FAITHFUL
 //    rounding of n/s (one of its two neighbours).  (The argument needs only
-//    e0^3 < 2^-56, i.e. e0 <= 2^-19: 2^4 below the documented bound.)
+//    e0 <= 2^-19.)  tests/test_division_model.py replays both forms in exact
+//    rational arithmetic.
 //    The check: r = fma(-q, s, n) is exact (q faithful; n = 0 or n >= 2^-969,
-//    s and q normal), r = s (n/s - q).  With yk = RN(y0 (1 + 2^-40) + ylo)
-//    (one fma),
+//    s and q normal), r = s (n/s - q).  With yk as above,
 //        t = fma(r, yk, q) = RN(q + (n/s - q) F),  F = s yk = (1 + d)(1 + 2^-40) + eps',
 //    |eps'| <= 2^-52, so 1 < F < 1 + 2^-39 (the fma forms r yk exactly, and t
 //    rounds once).  If q != RN(n/s),
@@ -38,9 +43,8 @@
 //    with dd_fix (q faithful: RN(n/s) is q or its neighbour, told apart by
 //    their exact residuals) instead of redoing the codeword; the demapper
 //    reruns the symbol on the exact path.
-//    Cost per normalisation pair: v_rcp_f64 + 4 shared + 5 per quotient (+ the
-//    fix, rare).  (Round 3's first form refined y0 by a Newton step first,
-//    y1 = y0 + y0 e, e1 = 1 - s y1, ylo = e1 y1: one instruction more per pair.)
+//    Cost per normalisation pair: v_rcp_f64 + 5 shared (4 without the Newton
+//    step) + 5 per quotient (+ the fix, rare).
 //
 // 2. div_rn (every other division: the decoders' exact re-decode, the
 //    non-FAST demap, k-means): any operands.  Finite normal operands with
@@ -65,7 +69,7 @@ struct DdRcp {
 };
 
 #ifndef KML_DD_NEWTON
-#define KML_DD_NEWTON 0
+#define KML_DD_NEWTON 1
 #endif
 __device__ __forceinline__ DdRcp dd_rcp(double s) {
   const double y0 = __builtin_amdgcn_rcp(s);

@@ -28,12 +28,21 @@ def mul(a, b):
     return rn(F(a) * F(b))
 
 
+NEWTON = True  # the shipped form (exact_div.hpp KML_DD_NEWTON); False: the Newton-free form
+
+
 def model(n, s, rel):
     y0 = rn(F(1) / F(s) * (1 + rel))  # v_rcp_f64 with relative error rel
-    e = fma(-y0, s, 1.0)
-    lo = mul(y0, fma(e, e, e))
-    k = fma(y0, 1.0 + 2.0 ** -40, lo)
-    q = fma(n, y0, mul(n, lo))
+    if NEWTON:
+        hi = fma(y0, fma(-y0, s, 1.0), y0)
+        lo = mul(fma(-hi, s, 1.0), hi)
+        k = mul(hi, 1.0 + 2.0 ** -40)
+    else:
+        hi = y0
+        e = fma(-y0, s, 1.0)
+        lo = mul(y0, fma(e, e, e))
+        k = fma(y0, 1.0 + 2.0 ** -40, lo)
+    q = fma(n, hi, mul(n, lo))
     t = fma(fma(-q, s, n), k, q)
     return q, t == q
 
@@ -44,7 +53,12 @@ def neighbours(x):
 
 
 def check(n, s, rel):
+    global NEWTON
     q, proven = model(n, s, rel)
+    NEWTON = not NEWTON  # both forms on every case
+    q2, proven2 = model(n, s, rel)
+    NEWTON = not NEWTON
+    assert not proven2 or q2 == rn(F(n) / F(s))
     exact = F(n) / F(s)
     r = rn(exact)
     lo, hi = neighbours(r)
