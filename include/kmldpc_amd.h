@@ -173,9 +173,10 @@ int kml_count_errors(kml_ctx *ctx, const uint8_t *uu, const uint8_t *uu_hat, int
 int kml_sim_generate(kml_ctx *ctx, double snr, uint64_t seed, uint64_t first_cw, int B);
 /* Receive the resident batch (blind or known-H) and accumulate the counters.
  * counters[8] (may be NULL) receives {err_bit, err_blk, tot_bit, tot_blk,
- * vn_phases, cn_phases, converged, redone} of this call (redone: codewords whose
- * fast decode met a quotient it could not prove correctly rounded and was
- * decoded again on the exact path; see DESIGN.md "Exact division").  If sync == 0 the call
+ * vn_phases, cn_phases, converged, redone} of this call (redone: codewords a
+ * FAST kernel deferred mid-decode to the exact kernel.  Unproven FAST
+ * quotients are settled in place (exact_div.hpp dd_fix), so this is 0 unless
+ * KML_FORCE_REDO=1 forces the path; see DESIGN.md "Bit-exactness strategy").  If sync == 0 the call
  * returns after enqueueing the work (counters must then be NULL); use
  * kml_sync to wait. */
 int kml_sim_decode(kml_ctx *ctx, double snr, int blind, uint64_t *counters, int sync);
@@ -303,7 +304,10 @@ int kml_div_probe(kml_ctx *ctx, const double *in, int n, double *out);
 /* Test hook: after the nth (0-based) cooperative BP launch from now, set that
  * kernel's abort word as a timed-out group barrier would (nth < 0: off).  The
  * call that owns the launch must then fail with KML_E_HIP, even when later
- * launches of the same call (chunks of a host-buffer decode) follow it. */
+ * launches of the same call (chunks of a host-buffer decode) follow it.
+ * nth = -2: raise the abort after the next cooperative launch AND fail that
+ * call at once, before its sync (the error-return path: the next call must
+ * start clean, not inherit the abort). */
 int kml_debug_inject_abort(kml_ctx *ctx, int nth);
 
 #ifdef __cplusplus

@@ -86,7 +86,9 @@ struct kml_ctx {
   int coop_groups = 0;      // cooperative BP groups (0: kernel not used)
   long long part_cut = 0;   // cut edges of the partition plan (partitioned cooperative kernel)
   bool coop_pending = false;  // a cooperative launch whose abort word is unchecked
+  bool coop_this_call = false;  // the current API call made a cooperative launch (fail() settles it)
   int inject_abort = -1;      // test hook (kml_debug_inject_abort): raise the abort after the n-th coop launch
+  bool inject_fail = false;   // test hook (kml_debug_inject_abort(-2)): ... and fail that call before its sync
   kml::RcclComm *comm = nullptr;  // counter all-reduce over the ranks (kml_comm_init)
   DBuf w_comm;
   DBuf w_defer;  // BP launches: codewords the FAST kernel leaves to the exact kernel (+ count)
@@ -114,8 +116,21 @@ struct kml_ctx {
 
 namespace {
 
+// An error return of a call that made a cooperative launch and will not reach
+// its sync(): the launch's abort word is settled here (waited for, dropped with
+// the call's error), so the next call's first launch clears it instead of
+// inheriting it (a stale timeout reported against a healthy call).  A pending
+// launch of an EARLIER call (kml_sim_decode with do_sync = 0) stays pending
+// for its own kml_sync.
 int fail(kml_ctx *c, int code, const std::string &msg) {
-  if (c) c->err = msg;
+  if (c) {
+    c->err = msg;
+    if (c->coop_pending && c->coop_this_call) {
+      if (c->stream) (void)hipStreamSynchronize(c->stream);
+      c->coop_pending = false;
+      c->coop_this_call = false;
+    }
+  }
   return code;
 }
 
@@ -402,14 +417,20 @@ int run_bp(kml_ctx *c, kml::BpLaunch a, int &slot_out, int reuse = -1) {
   // last sync(): a timeout in any launch before the check (e.g. chunk 0 of a
   // chunked host-buffer call) stays set until sync() reports it
   a.reset_abort = !c->coop_pending;
-  if (c->coop_groups > 0) c->coop_pending = true;
+  if (c->coop_groups > 0) c->coop_pending = c->coop_this_call = true;
   Timer t(c, "bp", slot, (double)a.B * 8.0 * c->code.cc_len);
   const char *msg = nullptr;
   hipError_t e = kml::launch_bp(c->dc, a, c->stream, &msg, &c->bp_family);
   t.stop();
   if (e != hipSuccess) return msg ? fail(c, KML_E_UNSUP, msg) : hip_fail(c, e, "bp launch");
   if (c->inject_abort >= 0 && c->coop_groups > 0 && c->inject_abort-- == 0)  // as if a group barrier timed out
+  {
     HIPCHK(c, kml::bp_coop_raise_abort(a, c->coop_groups, c->stream), "inject abort");
+    if (c->inject_fail) {
+      c->inject_fail = false;
+      return fail(c, KML_E_HIP, "injected failure after a cooperative launch (kml_debug_inject_abort)");
+    }
+  }
   slot_out = slot;
   return KML_OK;
 }
@@ -474,6 +495,7 @@ int sync(kml_ctx *c) {
 
 int need_gpu(kml_ctx *c) {
   if (c->device < 0 || !c->stream) return fail(c, KML_E_ARG, "host-only context (device < 0): no GPU operations");
+  c->coop_this_call = false;  // a new API call (every GPU entry point starts here)
   return KML_OK;
 }
 
@@ -1294,7 +1316,8 @@ int kml_comm_allreduce_f64(kml_ctx *c, double *vals, int n) { return comm_allred
 
 int kml_debug_inject_abort(kml_ctx *c, int nth) {
   if (!c) return KML_E_ARG;
-  c->inject_abort = nth;
+  c->inject_fail = nth == -2;
+  c->inject_abort = nth == -2 ? 0 : nth;
   return KML_OK;
 }
 

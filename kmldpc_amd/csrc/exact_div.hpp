@@ -23,9 +23,12 @@
 //    1/s, and
 //        q = fma(n, hi, RN(n ylo))
 //    rounds a value within 2^-66 relative of n/s once: q is a FAITHFUL
-//    rounding of n/s (one of its two neighbours).  (The argument needs only
-//    e0 <= 2^-19.)  tests/test_division_model.py replays both forms in exact
-//    rational arithmetic.
+//    rounding of n/s (one of its two neighbours).  Premise: e0 <= 2^-23 (the
+//    ISA's bound, which test_hardware_reciprocal_error asserts on the device
+//    and tests/test_division_model.py replays adversarially as +-2^-23 in
+//    exact rational arithmetic, both forms).  The argument itself has slack:
+//    the Newton form needs e0 <= 2^-20.1 (F > 1 below needs |e1| < 2^-40.2),
+//    the Newton-free form e0 <= 2^-22.3 (its e*^3 <= 2^-67).
 //    The check: r = fma(-q, s, n) is exact (q faithful; n = 0 or n >= 2^-969,
 //    s and q normal), r = s (n/s - q).  With yk as above,
 //        t = fma(r, yk, q) = RN(q + (n/s - q) F),  F = s yk = (1 + d)(1 + 2^-40) + eps',
@@ -64,8 +67,13 @@
 
 namespace kml {
 
+// The double-double reciprocal and the proof's scaled reciprocal:
+//   KML_DD_NEWTON = 1 (shipped): hi = y1 = y0 + y0 RN(1 - s y0), lo = RN(e1 y1)
+//                                with e1 = RN(1 - s y1), k = RN(y1 (1 + 2^-40));
+//   KML_DD_NEWTON = 0:           hi = y0, lo = RN(y0 RN(e + e^2)) with
+//                                e = RN(1 - s y0), k = RN(y0 (1 + 2^-40) + lo).
 struct DdRcp {
-  double hi, lo, k;  // y0, RN(y0 (e + e^2)), RN(y0 (1 + 2^-40) + lo)
+  double hi, lo, k;
 };
 
 #ifndef KML_DD_NEWTON

@@ -170,6 +170,53 @@ def test_bench_two_ranks_gloo(data_dir, tmp_path):
     ctx.close()
 
 
+@pytest.mark.timeout(400)
+def test_bench_eight_ranks_gloo(data_dir, tmp_path):
+    """`bench.py --gpus 8` with 8 rank processes sharing this GPU (gloo
+    counters): the N = 8 rank logic of the driver's scaling run (child
+    torchrun, shard offsets rank * B, barrier, max-over-ranks timing, counter
+    all-reduce) with only the RCCL transport left out.  Rank 0's counters equal
+    one decode of the whole index range [0, 8 B) (simulator.cc:35-42, 86-100)."""
+    B, W = 512, 8
+    line = _bench(["--gpus", str(W), "--dist-backend", "gloo", "--steps", "2", "--warmup", "1", "--batch", str(B),
+                   "--no-cpu-baseline", "--no-ber-match", "--full-loop-batches", "1"], timeout=380)
+    assert line["n_gpus"] == W and line["ranks"] == W and line["dist_backend"].startswith("gloo counters")
+    assert len(line["rank_ms_per_step"]) == W and line["config"]["global_batch"] == W * B
+    assert line["ms_per_step"] == pytest.approx(max(line["rank_ms_per_step"]), rel=1e-6)
+    st = line["stats"]
+    assert st["codewords"] == W * B
+    ctx = _ctx(data_dir, tmp_path, "PEG2304regular0.5.txt", "2bits_QPSK.txt")
+    ctx.sim_generate(2.0, W * B, seed=17, first_cw=0)
+    c = ctx.sim_decode(2.0, blind=False)
+    assert round(st["fer"] * W * B) == c["err_blk"]
+    assert round(st["ber"] * c["tot_bit"]) == c["err_bit"]
+    ctx.close()
+
+
+@pytest.mark.timeout(400)
+def test_simulate_eight_ranks_gloo_matches_single_rank(data_dir, tmp_path):
+    """kmldpc_amd.simulate under torchrun --nproc-per-node 8 (ranks sharing this
+    GPU, gloo counters): blind PEG2304 at two SNR points with an error limit
+    that lands inside a round and a block limit no round size divides.  The
+    BER / FER tables equal the single-process run's (the stop rule is exact for
+    any world, simulate.cpp kml_sweep_point; simulator.cc:117)."""
+    cfg = tmp_path / "config.toml"
+    write_config(str(cfg), data_dir, "PEG2304regular0.5.txt", "2bits_QPSK.txt", known=False, snr=1.0, snr_max=2.0,
+                 snr_step=1.0, max_blocks=2900, max_err=333, thread_blocks=1000)
+    env = dict(os.environ, PYTHONPATH=REPO, KML_BATCH="96", KML_SEED="5", KML_DIST_BACKEND="gloo",
+               OMP_NUM_THREADS="1")
+    r1 = subprocess.run([sys.executable, "-m", "kmldpc_amd.simulate", str(cfg)], cwd=tmp_path, env=env,
+                        capture_output=True, text=True, timeout=300)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    r8 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+                         "--master-addr=127.0.0.1", "--master-port=29547", "-m", "kmldpc_amd.simulate", str(cfg)],
+                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=360)
+    assert r8.returncode == 0, r8.stderr[-3000:]
+    b1, f1 = _tables(r1.stdout)
+    b8, f8 = _tables(r8.stdout)
+    assert b1 == b8 and f1 == f8 and len(b1) == 2
+
+
 def test_bench_one_rank_rccl_group(data_dir):
     """The RCCL leg on hardware: `bench.py --gpus 1 --force-dist` runs one rank
     under torch.distributed.run (gloo rendezvous), builds the library's RCCL
