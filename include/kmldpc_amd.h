@@ -102,7 +102,8 @@ void kml_destroy(kml_ctx *ctx);
 const char *kml_last_error(const kml_ctx *ctx);
 int kml_abi_version(void);
 /* Name of the BP kernel family the context last launched ("bp_regular_kernel",
- * "bp_irregular_kernel", "bp_coop_kernel", "bp_kernel"; "" before any decode). */
+ * "bp_irregular_kernel", "bp_part_kernel" (the partitioned cooperative kernel,
+ * PEG8064), "bp_coop_kernel", "bp_kernel"; "" before any decode). */
 const char *kml_bp_kernel(const kml_ctx *ctx);
 
 int kml_dims(const kml_ctx *ctx, int32_t *dims /* [KML_DIM_COUNT] */);

@@ -218,6 +218,12 @@ __device__ __noinline__ void div_stats_record(bool ok, bool c0, bool c1, double 
   }
 #endif
 
+// KML_DIV_NOPROOF = 1 (A/B measurement builds only, `make variant`): the FAST
+// VN quotients skip dd_check / dd_fix, i.e. faithful but unproven — the price
+// of the proof per kernel family, never a shipped build (the parity tests fail).
+#ifndef KML_DIV_NOPROOF
+#define KML_DIV_NOPROOF 0
+#endif
 // DEFER (FAST VN only): a quotient the check cannot prove is left faithful and
 // sets sus, for a caller that then reruns the whole column with DEFER = false
 // (one rare branch per column instead of one per normalisation).
@@ -234,6 +240,9 @@ __device__ __forceinline__ void div2(double n0, double n1, double s, double &q0,
     const DdRcp y = dd_rcp(s);
     q0 = dd_quot(n0, y);
     q1 = dd_quot(n1, y);
+#if KML_DIV_NOPROOF  // (A/B measurement builds only: faithful, NOT proven correctly rounded)
+    return;
+#endif
     const bool c0 = dd_check(n0, s, q0, y), c1 = dd_check(n1, s, q1, y);
 #if KML_DIV_STATS
     div_stats_record(true, c0, c1, n0, n1, s, q0, q1);

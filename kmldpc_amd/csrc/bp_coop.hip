@@ -81,8 +81,12 @@ __device__ __forceinline__ unsigned vaddr_slot(int v) { return (unsigned)(v & 0x
 
 // LDS of the partitioned kernel: the member's row slots, its mirror slots, and
 // every column's hard decision.
+// kPartDummy slots past the mirrors: the target of the branch-free tagged
+// stores of inactive lanes (a lane past the member's columns or rows), which
+// compute throw-away messages.
+constexpr int kPartDummy = 7;
 size_t part_lds_bytes(const DevCode &c) {
-  return ((size_t)c.M / kPartG * 6 + (size_t)c.pt_mirror) * 16 + (size_t)c.N;
+  return ((size_t)c.M / kPartG * 6 + (size_t)c.pt_mirror + kPartDummy) * 16 + (size_t)c.N;
 }
 
 #ifndef KML_POLL_SLEEP  // (A/B) s_sleep between the tagged mailbox polls
@@ -93,7 +97,15 @@ constexpr long long kSpinLimit = 20000000;  // ~1 s of s_sleep(1) polls
 // The tagged mailboxes (bp_part_kernel) follow the barrier-exchange ones in
 // the group's E double2 of scratch: 3 ncut doubles, rounded to 16 bytes, then
 // another 3 ncut.
-__host__ __device__ constexpr bool part_tagged_fits(int E, int ncut) { return 6LL * ncut + 2 <= 2LL * E; }
+// The branch-free tagged stores address a row slot's (absent) v2c entry as
+// kMbOob (entry 0x7FFF, byte offset 0x7FFF0) and a row slot's c2v entry as
+// kMbOobOff: both out of the mailbox buffer's range (24 ncut bytes), which the
+// hardware's range check drops, so ncut <= 0x7FFF0 / 24.
+constexpr int kMbOob = 0x7FFF;
+constexpr unsigned kMbOobOff = 0x80000000u;
+__host__ __device__ constexpr bool part_tagged_fits(int E, int ncut) {
+  return 6LL * ncut + 2 <= 2LL * E && 24LL * ncut <= 16LL * kMbOob;
+}
 // byte offset of the deferred-codeword count in the sync block (past the abort word)
 constexpr size_t part_defer_offset(int groups) { return sizeof(GroupSync) * (size_t)groups + 16; }
 
@@ -982,7 +994,8 @@ __device__ __forceinline__ int part_iterations_tagged(
     unsigned *abort, unsigned char *smem, uint8_t *dec, int NG, __amdgpu_buffer_rsrc_t tb, unsigned tb_c2v,
     const int (&vaddr)[RV][3],
     const bool (&vact)[RV], const double (&pv)[RV], const int (&crow)[RC],
-    const int (&cbase)[RC], const int (&crx)[RC], const bool (&cact)[RC], const int (&xr)[RX], const int (&xc)[RX],
+    const int (&cbase)[RC], const int (&crx)[RC], const int (&cwb)[RC], const bool (&cact)[RC], const int (&xr)[RX],
+    const int (&xc)[RX],
     int odd, int &iter_out, bool &conv_out, int &pcnt_out, int &decbuf_out, bool sus0 = false) {
   constexpr int DV = 3, DC = 6, H = 3, NW = T / 64;
   const int tid = threadIdx.x;
@@ -1061,14 +1074,11 @@ __device__ __forceinline__ int part_iterations_tagged(
             div2<true, true>(t0, t1, t0 + t1, q0, q1, sus);
           else
             div2<true>(t0, t1, t0 + t1, q0, q1, sus);
-          if (vact[r]) {
-            const int x1 = (int)((unsigned)vaddr[r][k] >> 17);  // mailbox index + 1 of a cut edge, 0 for a row slot
-            if (x1) {
-              const unsigned tb_tag = tag ? kTagHi : 0u;
-              mb_st128(tb, (unsigned)(x1 - 1) * 16, or_hi(q0, tb_tag | hdb), or_hi(q1, tb_tag));
-            } else {
-              *reinterpret_cast<double2 *>(smem + vaddr_slot(vaddr[r][k])) = make_double2(or_hi(q0, hdb), q1);
-            }
+          {  // branch-free (see vaddr): the mailbox entry (dropped for a row slot) and the LDS slot
+            const unsigned va = (unsigned)vaddr[r][k];
+            const unsigned tb_tag = tag ? kTagHi : 0u;
+            mb_st128(tb, (va >> 17) << 4, or_hi(q0, tb_tag | hdb), or_hi(q1, tb_tag));
+            *reinterpret_cast<double2 *>(smem + vaddr_slot(vaddr[r][k])) = make_double2(or_hi(q0, hdb), q1);
           }
           if (k > 0) {
             const double c0 = c0c[k];
@@ -1202,22 +1212,18 @@ __device__ __forceinline__ int part_iterations_tagged(
             const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
             const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
             const double q = clip_c2v<true>(div1<true, true>(t0, t0 + t1));
-            if (cact[r]) {
-              // the store's addresses are recomputed here from opaque copies
-              // of crx and odd: hoisted out of the iteration loop, the 2 x 3
-              // per-lane mailbox offsets, masks and LDS addresses were spilled,
-              // and each c2v store waited on a scratch reload (s_waitcnt
-              // vmcnt(0) behind every outstanding store)
-              int cr = crx[r], od = odd;
-              asm volatile("" : "+v"(cr), "+v"(od));
-              const int e = od ? st : DC - 1 - st;  // the edge this c2v belongs to
-              const int mask = cr & 0x3F;  // bit 7: the row's c2v half (kernel setup)
-              if ((mask >> e) & 1) {
-                const int x = (cr >> 8) + __popc(mask & ((1 << e) - 1));
-                mb_st64(tb, tb_c2v + (unsigned)x * 8, or_hi(q, tag ? kTagHi : 0u));
-              } else {
-                *reinterpret_cast<double *>(smem + cbase[r] + e * 16 + ((cr >> 4) & 8)) = q;
-              }
+            {
+              // branch-free: the mailbox entry of a cut edge (a row slot's
+              // offset is out of the buffer's range: dropped) and the row
+              // slot's c2v half (a cut edge's is never read; an inactive lane
+              // writes the dummy slots).  Offsets from crx at the store: kept
+              // per lane across the loop they spilled at the 128-VGPR limit.
+              const unsigned cr = (unsigned)crx[r];
+              const unsigned e = odd ? st : DC - 1 - st;  // the edge this c2v belongs to
+              const unsigned cut = __builtin_amdgcn_ubfe(cr, e, 1);
+              const unsigned x = __popc(__builtin_amdgcn_ubfe(cr, 0, e)) + (cr >> 8);
+              mb_st64(tb, cut ? tb_c2v + x * 8 : kMbOobOff, or_hi(q, tag ? kTagHi : 0u));
+              *reinterpret_cast<double *>(smem + cwb[r] + e * 16) = q;
             }
           }
         }
@@ -1295,9 +1301,15 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
   const unsigned tb_c2v = 16u * (unsigned)c.pt_ncut;
   uint8_t *gc = gcch + (size_t)group * c.N;
   const int nslots = EG + c.pt_mirror;
-  uint8_t *dec = smem + (size_t)nslots * 16;  // N hard decisions, plan order
+  uint8_t *dec = smem + (size_t)(nslots + kPartDummy) * 16;  // N hard decisions, plan order
 
-  // vaddr: (mailbox index + 1 of a cut edge, 0 for a row slot) << 17 | (2 LDS slot + c2v half)
+  // vaddr: (v2c mailbox index of a cut edge, kMbOob for a row slot) << 17 |
+  // (2 LDS slot + c2v half).  The tagged kernel stores every v2c to both the
+  // LDS slot and the mailbox entry, branch-free: a row slot's mailbox store
+  // lands out of the buffer's range (dropped by the hardware's range check),
+  // a cut edge's LDS store in its mirror slot (whose c2v the column has
+  // already read).  An inactive lane (past the member's columns) reads and
+  // writes the dummy slots.
   int vaddr[RV][DV], vpos[RV];
   bool vact[RV];
 #pragma unroll
@@ -1308,11 +1320,14 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
 #pragma unroll
     for (int k = 0; k < DV; ++k)
     {
-      const int sl = c.pt_vaddr[vpos[r] * DV + k] >> 4;
-      vaddr[r][k] = ((c.pt_vx[vpos[r] * DV + k] + 1) << 17) | (2 * sl + part_c2v_half(sl, EG, DC));
+      // (an inactive lane reads the upper half of its dummy slot: the q1 word
+      // it wrote itself, a probability)
+      const int sl = vact[r] ? c.pt_vaddr[vpos[r] * DV + k] >> 4 : nslots + k;
+      const int vx = vact[r] ? c.pt_vx[vpos[r] * DV + k] : -1;
+      vaddr[r][k] = ((vx >= 0 ? vx : kMbOob) << 17) | (2 * sl + (vact[r] ? part_c2v_half(sl, EG, DC) : 1));
     }
   }
-  int crow[RC], cbase[RC], crx[RC];
+  int crow[RC], cbase[RC], crx[RC], cwb[RC];
   bool cact[RC];
 #pragma unroll
   for (int r = 0; r < RC; ++r) {
@@ -1322,7 +1337,9 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
     const int row = c.pt_cn[member * MG + li];
     crow[r] = row;
     cbase[r] = li * DC * 16;
-    crx[r] = c.pt_rx[member * MG + li] | (part_c2v_half(li * DC, EG, DC) << 7);
+    crx[r] = cact[r] ? c.pt_rx[member * MG + li] | (part_c2v_half(li * DC, EG, DC) << 7) : 0;
+    // c2v write base: the row's slots + its c2v half, or the dummy slots
+    cwb[r] = cact[r] ? cbase[r] + part_c2v_half(li * DC, EG, DC) * 8 : nslots * 16;
   }
   int xr[RX], xc[RX];
   {
@@ -1385,7 +1402,7 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
       ok = ok && fast_prior_ok(pv[r], plo);
     }
     // InitMsg: row slots and mirror slots (c2v = 0.5)
-    for (int e = tid; e < nslots; e += T) reinterpret_cast<double2 *>(smem)[e] = make_double2(0.5, 0.5);
+    for (int e = tid; e < nslots + kPartDummy; e += T) reinterpret_cast<double2 *>(smem)[e] = make_double2(0.5, 0.5);
     if (__ballot(!ok) != 0 && (tid & 63) == 0)
       __hip_atomic_fetch_or(&gs->nofast, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;
@@ -1401,7 +1418,7 @@ __global__ __launch_bounds__(T) void bp_part_kernel(DevCode c, BpLaunch a, Group
       }
       const int st = part_iterations_tagged<kG, T, RV, RC, RX, SYN>(a, c.M, cw, gs, g, &sfail, &sdead, member, abort,
                                                                    smem, dec, NG, tb, tb_c2v, vaddr, vact, pv, crow,
-                                                                   cbase, crx, cact, xr, xc, odd, iter, conv, pcnt,
+                                                                   cbase, crx, cwb, cact, xr, xc, odd, iter, conv, pcnt,
                                                                    decbuf, (fast_allowed & 2) != 0);
       if (st < 0) return;
       if (st == 1) {  // an unproven quotient: redone by the exact launch (every member took this branch)
@@ -1667,7 +1684,7 @@ int bp_part_group_size(int N, int M, int E, int dv_max, int dc_max, int regular)
 }
 
 bool part_plan_fits(int N, int M, int E, int ncut, int mirror_max, int xmax) {
-  const long long lds = ((long long)M / kPartG * 6 + mirror_max) * 16 + N;
+  const long long lds = ((long long)M / kPartG * 6 + mirror_max + kPartDummy) * 16 + N;
   return lds <= 160 * 1024 && 3LL * ncut <= 2LL * E && xmax <= 2 * 1024;
 }
 

@@ -180,6 +180,9 @@ int upload_code(kml_ctx *c) {
   kml::PartitionPlan part;
   const int part_G = kml::bp_part_group_size(L.N, L.M, L.E, L.dv_max, L.dc_max, regular);
   if (part_G > 0 && !kml::plan_partition(L, part_G, part)) part.G = 0;
+  if (part.G && getenv("KML_PLAN_VERBOSE"))
+    fprintf(stderr, "partition plan: G %d, %d cut edges, mirrors <= %d, VN bank model cost %lld -> %lld\n", part.G,
+            part.ncut, part.mirror_max, part.anneal_initial, part.anneal_final);
   int part_xmax = 0;
   for (int m = 0; part.G && m < part.G; m++)
     part_xmax = std::max({part_xmax, part.xr_ptr[m + 1] - part.xr_ptr[m], part.xc_ptr[m + 1] - part.xc_ptr[m]});

@@ -212,9 +212,131 @@ void assign_majority(const std::vector<int32_t> &ptr, const std::vector<int32_t>
     }
 }
 
+// The VN phase's LDS bank model (bp_regular's, above): position p's column
+// stores its k-th v2c slot with ds_write_b128 (8-lane groups: 8 bins of 16 B
+// mod 128 B, bin wb) and reads its k-th c2v with ds_read_b64 (32-lane halves:
+// 32 bins of 8 B mod 256 B, bin rb).  Anneals the column order ord[lo, hi)
+// (all columns of one degree) against the summed excess group maxima.
+// Returns (initial cost, final cost).
+std::pair<long long, long long> anneal_vn_order(std::vector<int32_t> &ord, int lo, int hi, int dv,
+                                                const std::vector<uint8_t> &wb, const std::vector<uint8_t> &rb,
+                                                uint64_t seed, long long iters) {
+  const int n = hi - lo;
+  const int nW = (n + 7) / 8, nR = (n + 31) / 32;
+  std::vector<uint16_t> wc((size_t)nW * dv * 8, 0), rc((size_t)nR * dv * 32, 0);
+  std::vector<int> wmax((size_t)nW * dv, 0), rmax((size_t)nR * dv, 0);
+  auto wcnt = [&](int g, int k) { return &wc[((size_t)g * dv + k) * 8]; };
+  auto rcnt = [&](int g, int k) { return &rc[((size_t)g * dv + k) * 32]; };
+  auto gmax = [](const uint16_t *c, int m) {
+    int x = 0;
+    for (int i = 0; i < m; i++) x = std::max(x, (int)c[i]);
+    return x;
+  };
+  for (int p = 0; p < n; p++)
+    for (int k = 0; k < dv; k++) {
+      wcnt(p / 8, k)[wb[(size_t)ord[lo + p] * dv + k]]++;
+      rcnt(p / 32, k)[rb[(size_t)ord[lo + p] * dv + k]]++;
+    }
+  long long cost = 0;
+  for (int g = 0; g < nW; g++)
+    for (int k = 0; k < dv; k++) cost += (wmax[(size_t)g * dv + k] = gmax(wcnt(g, k), 8)) - 1;
+  for (int g = 0; g < nR; g++)
+    for (int k = 0; k < dv; k++) cost += (rmax[(size_t)g * dv + k] = gmax(rcnt(g, k), 32)) - 1;
+  const long long c0 = cost;
+  Xorshift rng{seed};
+  double temp = 1.0;
+  const double cool = std::pow(0.05, 1.0 / (double)std::max(iters, 1LL));
+  auto move = [&](int p, int col, int sign) {
+    for (int k = 0; k < dv; k++) {
+      wcnt(p / 8, k)[wb[(size_t)col * dv + k]] += sign;
+      rcnt(p / 32, k)[rb[(size_t)col * dv + k]] += sign;
+    }
+  };
+  auto group_delta = [&](int a, int b, bool commit) {
+    long long d = 0;
+    for (int k = 0; k < dv; k++) {
+      const int ga = a / 8, gb = b / 8;
+      int m = gmax(wcnt(ga, k), 8);
+      d += m - wmax[(size_t)ga * dv + k];
+      if (commit) wmax[(size_t)ga * dv + k] = m;
+      if (gb != ga) {
+        m = gmax(wcnt(gb, k), 8);
+        d += m - wmax[(size_t)gb * dv + k];
+        if (commit) wmax[(size_t)gb * dv + k] = m;
+      }
+      const int ra = a / 32, rb2 = b / 32;
+      m = gmax(rcnt(ra, k), 32);
+      d += m - rmax[(size_t)ra * dv + k];
+      if (commit) rmax[(size_t)ra * dv + k] = m;
+      if (rb2 != ra) {
+        m = gmax(rcnt(rb2, k), 32);
+        d += m - rmax[(size_t)rb2 * dv + k];
+        if (commit) rmax[(size_t)rb2 * dv + k] = m;
+      }
+    }
+    return d;
+  };
+  for (long long it = 0; it < iters; it++, temp *= cool) {
+    const int a = (int)(rng.next() % (uint64_t)n), b = (int)(rng.next() % (uint64_t)n);
+    if (a / 8 == b / 8) continue;
+    const int ca = ord[lo + a], cb = ord[lo + b];
+    move(a, ca, -1);
+    move(b, cb, -1);
+    move(a, cb, +1);
+    move(b, ca, +1);
+    const long long d = group_delta(a, b, false);
+    if (d <= 0 || rng.uniform() < std::exp(-(double)d / temp)) {
+      group_delta(a, b, true);
+      std::swap(ord[lo + a], ord[lo + b]);
+      cost += d;
+    } else {
+      move(a, cb, -1);
+      move(b, ca, -1);
+      move(a, ca, +1);
+      move(b, cb, +1);
+    }
+  }
+  return {c0, cost};
+}
+
 }  // namespace
 
+#ifndef KML_PART_ANNEAL  // (A/B) 0: members' columns in index order
+#define KML_PART_ANNEAL 1
+#endif
+
+static bool plan_partition_uncached(const LdpcCode &L, int G, PartitionPlan &out);
+
+// Cached like plan_regular_layout: a pure function of the graph, and the
+// annealing takes ~1 s.
 bool plan_partition(const LdpcCode &L, int G, PartitionPlan &out) {
+  struct Entry {
+    std::vector<int32_t> row_col, col_slot;
+    int G;
+    bool ok;
+    PartitionPlan plan;
+  };
+  static std::mutex mu;
+  static std::vector<std::unique_ptr<Entry>> cache;
+  std::lock_guard<std::mutex> g(mu);
+  for (auto &e : cache)
+    if (e->G == G && e->row_col == L.row_col && e->col_slot == L.col_slot) {
+      out = e->plan;
+      return e->ok;
+    }
+  auto e = std::make_unique<Entry>();
+  e->row_col = L.row_col;
+  e->col_slot = L.col_slot;
+  e->G = G;
+  e->ok = plan_partition_uncached(L, G, e->plan);
+  out = e->plan;
+  const bool ok = e->ok;
+  if (cache.size() >= 4) cache.erase(cache.begin());
+  cache.push_back(std::move(e));
+  return ok;
+}
+
+static bool plan_partition_uncached(const LdpcCode &L, int G, PartitionPlan &out) {
   const int M = L.M, N = L.N, E = L.E;
   if (G <= 0 || M % G || N % G || !L.dv_max || !L.dc_max) return false;
   for (int j = 0; j < N; j++)
@@ -279,7 +401,7 @@ bool plan_partition(const LdpcCode &L, int G, PartitionPlan &out) {
     assign_majority(L.row_ptr, row_cols, cpart, G, MG, rng, rpart);
   }
 
-  // member orders: columns and rows by index
+  // member orders: rows by index, columns by index (annealed below)
   out.G = G;
   out.MG = MG;
   out.NG = NG;
@@ -291,22 +413,20 @@ bool plan_partition(const LdpcCode &L, int G, PartitionPlan &out) {
     for (int i = 0; i < M; i++)
       if (best_r[i] == g) out.cn.push_back(i);
   }
-  out.pos.assign(N, 0);
-  for (int p = 0; p < N; p++) out.pos[out.vn[p]] = p;
   std::vector<int32_t> row_at(M);
   for (int p = 0; p < M; p++) row_at[out.cn[p]] = p;
   const int EG = MG * dc;
 
   // cut edges, sorted by (row owner, partitioned row slot)
   struct Cut {
-    int R, S, slot, col_pos, k;
+    int R, S, slot, col, k;
   };
   std::vector<Cut> cuts;
   for (int p = 0; p < N; p++) {
     const int j = out.vn[p];
     for (int e = L.col_ptr[j], k = 0; e < L.col_ptr[j + 1]; e++, k++) {
       const int s = L.col_slot[e], r = slot_row[s];
-      if (best_r[r] != best_c[j]) cuts.push_back({best_r[r], best_c[j], row_at[r] * dc + (s - L.row_ptr[r]), p, k});
+      if (best_r[r] != best_c[j]) cuts.push_back({best_r[r], best_c[j], row_at[r] * dc + (s - L.row_ptr[r]), j, k});
     }
   }
   std::sort(cuts.begin(), cuts.end(), [](const Cut &a, const Cut &b) {
@@ -335,20 +455,52 @@ bool plan_partition(const LdpcCode &L, int G, PartitionPlan &out) {
     out.xr_ptr.push_back((int32_t)out.xr.size());
     out.xc_ptr.push_back((int32_t)out.xc.size());
   }
-  // per-edge LDS addresses of the VN phase: own row slot, or the mirror slot
-  out.vaddr.assign((size_t)N * dv, 0);
-  for (int p = 0; p < N; p++) {
-    const int j = out.vn[p], g = best_c[j];
+  // per-edge LDS addresses of the VN phase, per column: own row slot, or the
+  // mirror slot
+  std::vector<int32_t> caddr((size_t)N * dv, 0), cvx((size_t)N * dv, -1);
+  for (int j = 0; j < N; j++) {
+    const int g = best_c[j];
     for (int e = L.col_ptr[j], k = 0; e < L.col_ptr[j + 1]; e++, k++) {
       const int s = L.col_slot[e], r = slot_row[s];
-      if (best_r[r] == g) out.vaddr[(size_t)p * dv + k] = ((row_at[r] - g * MG) * dc + (s - L.row_ptr[r])) * 16;
+      if (best_r[r] == g) caddr[(size_t)j * dv + k] = ((row_at[r] - g * MG) * dc + (s - L.row_ptr[r])) * 16;
     }
   }
+  for (size_t x = 0; x < cuts.size(); x++) {
+    caddr[(size_t)cuts[x].col * dv + cuts[x].k] = (EG + mirror_of[x]) * 16;
+    cvx[(size_t)cuts[x].col * dv + cuts[x].k] = (int32_t)x;
+  }
+  // the columns' lane positions within each member: annealed against the VN
+  // phase's bank conflicts (write bins of the slot, read bins of the c2v half:
+  // bp_coop.hip part_c2v_half — bit 2 of the row for row slots, of the slot
+  // index for mirror slots)
+  if (KML_PART_ANNEAL) {
+    std::vector<uint8_t> wb((size_t)N * dv), rb((size_t)N * dv);
+    for (int j = 0; j < N; j++)
+      for (int k = 0; k < dv; k++) {
+        const int a = caddr[(size_t)j * dv + k], sl = a >> 4;
+        const int half = sl < EG ? ((sl / dc) >> 2) & 1 : (sl >> 2) & 1;
+        wb[(size_t)j * dv + k] = (uint8_t)((a >> 4) & 7);
+        rb[(size_t)j * dv + k] = (uint8_t)(((a + 8 * half) >> 3) & 31);
+      }
+    out.anneal_initial = out.anneal_final = 0;
+    for (int g = 0; g < G; g++) {
+      const auto c = anneal_vn_order(out.vn, g * NG, (g + 1) * NG, dv, wb, rb, 0x9E3779B97F4A7C15ull + (uint64_t)g,
+                                     300LL * NG * dv);
+      out.anneal_initial += c.first;
+      out.anneal_final += c.second;
+    }
+  }
+  out.pos.assign(N, 0);
+  for (int p = 0; p < N; p++) out.pos[out.vn[p]] = p;
+  out.vaddr.assign((size_t)N * dv, 0);
   out.vx.assign((size_t)N * dv, -1);
+  for (int p = 0; p < N; p++)
+    for (int k = 0; k < dv; k++) {
+      out.vaddr[(size_t)p * dv + k] = caddr[(size_t)out.vn[p] * dv + k];
+      out.vx[(size_t)p * dv + k] = cvx[(size_t)out.vn[p] * dv + k];
+    }
   out.rx.assign(M, 0);
   for (size_t x = 0; x < cuts.size(); x++) {
-    out.vaddr[(size_t)cuts[x].col_pos * dv + cuts[x].k] = (EG + mirror_of[x]) * 16;
-    out.vx[(size_t)cuts[x].col_pos * dv + cuts[x].k] = (int32_t)x;
     const int P = cuts[x].slot / dc, e = cuts[x].slot % dc;  // plan row index, edge position in the row
     if (!(out.rx[P] & 0xFF)) out.rx[P] = (int32_t)(x << 8);
     out.rx[P] |= 1 << e;

@@ -68,6 +68,7 @@ struct PartitionPlan {
   std::vector<int32_t> vx;  // 3N: [p*dv + k] = mailbox index x of that edge when it is cut, else -1
   std::vector<int32_t> rx;  // M, plan order: (x of the row's first cut edge << 8) | mask of its cut
                             // edges by position in the row (0 when none are cut)
+  long long anneal_initial = 0, anneal_final = 0;  // VN bank-conflict model cost before / after annealing
 };
 
 // False when the code is not regular or M, N are not multiples of G.
