@@ -49,7 +49,8 @@ KERNEL_NOTES = {
     "bp_regular_kernel": "sum-product BP, messages LDS-resident",
     "bp_irregular_kernel": "sum-product BP, irregular degrees, messages LDS-resident",
     "bp_coop_kernel": "sum-product BP, 4 workgroups per codeword, messages in L2",
-    "bp_part_kernel": "sum-product BP, 4 workgroups per codeword, partitioned LDS slots + cut-edge mailboxes",
+    "bp_part_kernel": "sum-product BP, partitioned LDS slots + cut-edge mailboxes: 8 workgroups per codeword, two "
+                      "codewords in flight per group (bp_part2_kernel)",
     "bp_kernel": "sum-product BP, generic",
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec

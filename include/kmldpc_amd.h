@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define KML_ABI_VERSION 1
+#define KML_ABI_VERSION 2  /* 2: KML_DIM_PART_G (KML_DIM_COUNT 13) */
 
 enum {
   KML_OK = 0,
@@ -87,7 +87,8 @@ enum {
   KML_DIM_KC = 9,       /* constellation points */
   KML_DIM_S = 10,       /* symbols per codeword */
   KML_DIM_BP_LDS = 11,  /* 1 if the decoder keeps messages in LDS */
-  KML_DIM_COUNT = 12
+  KML_DIM_PART_G = 12,  /* workgroups per codeword of the partitioned decoder (8 or 4), 0 when not used */
+  KML_DIM_COUNT = 13
 };
 
 /* Create a context from a reference config.toml.  Relative matrix_file /

@@ -46,6 +46,12 @@ inline void check(kml_ctx *ctx, int rc) {
 }
 
 inline kml_ctx *open_ctx(const std::string &config_path, int device) {
+  if (kml_abi_version() != KML_ABI_VERSION) {  // a library built from another header (kml_dims' array length, ...)
+    lab::logger::ERROR("kmldpc_amd: library ABI " + std::to_string(kml_abi_version()) + ", header ABI " +
+                           std::to_string(KML_ABI_VERSION) + ": rebuild against the library's include/kmldpc_amd.h",
+                       true);
+    exit(-1);
+  }
   kml_ctx *ctx = nullptr;
   const int rc = kml_create(config_path.c_str(), nullptr, device, &ctx);
   if (rc != KML_OK) {

@@ -186,7 +186,7 @@ int upload_code(kml_ctx *c) {
   int part_xmax = 0;
   for (int m = 0; part.G && m < part.G; m++)
     part_xmax = std::max({part_xmax, part.xr_ptr[m + 1] - part.xr_ptr[m], part.xc_ptr[m + 1] - part.xc_ptr[m]});
-  if (part.G && !kml::part_plan_fits(L.N, L.M, L.E, part.ncut, part.mirror_max, part_xmax)) part.G = 0;
+  if (part.G && !kml::part_plan_fits(part.G, L.N, L.M, L.E, part.ncut, part.mirror_max, part_xmax)) part.G = 0;
   reserve(part.vn.size() * 4);
   reserve(part.cn.size() * 4);
   reserve(part.pos.size() * 4);
@@ -263,7 +263,8 @@ int upload_code(kml_ctx *c) {
   d.irr_slots = irr.n_slots;
   d.pt_ncut = part.ncut;
   d.pt_mirror = part.mirror_max;
-  for (int m = 0; m < 4; m++) {
+  d.pt_pairs = part.all_pairs ? 1 : 0;
+  for (int m = 0; m < 8; m++) {
     d.pt_xr_n[m] = m < part.G ? part.xr_ptr[m + 1] - part.xr_ptr[m] : 0;
     d.pt_xc_n[m] = m < part.G ? part.xc_ptr[m + 1] - part.xc_ptr[m] : 0;
   }
@@ -969,6 +970,7 @@ int kml_dims(const kml_ctx *c, int32_t *d) {
   tmp.E = L.E;
   tmp.N = L.N;
   d[KML_DIM_BP_LDS] = kml::bp_uses_lds(tmp) ? 1 : 0;
+  d[KML_DIM_PART_G] = c->dc.pt_G;
   return KML_OK;
 }
 

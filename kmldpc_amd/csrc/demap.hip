@@ -35,6 +35,9 @@ namespace {
 // 64QAM: the 64 probabilities of a symbol stay in registers (280 VGPRs
 // unconstrained, one wave per SIMD); KML_DEMAP64_WAVES = 2 caps the kernel at
 // 256 so two waves per SIMD hide the exp table loads and the dependent chains
+#ifndef KML_EXPTAB_BANKED  // (A/B) 0: the 64QAM demap_kernel reads the plain exp table
+#define KML_EXPTAB_BANKED 1
+#endif
 #ifndef KML_DEMAP64_WAVES
 #define KML_DEMAP64_WAVES 2
 #endif
@@ -44,7 +47,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? K
                                                     const int32_t *__restrict__ h_sel, double var, int B,
                                                     double *__restrict__ p0, DemapDefer d) {
   __shared__ double cl[2 << MB];  // the constellation, read with uniform LDS loads
-  __shared__ uint64_t etab[256];
+  // the exp table: bank-private copies for 64QAM (64 exps per symbol), the
+  // plain table otherwise (demap_common.hpp stage_exp_table_banked)
+  constexpr int ES = (MB >= 6 && KML_EXPTAB_BANKED) ? kExpBanked : 2;
+  __shared__ uint64_t etab[ES == 2 ? 256 : 128 * kExpBanked];
   const long long n = (long long)B * S;
   long long todo = n;
   bool listed = false;
@@ -55,8 +61,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? K
     if (listed) todo = cnt;
   }
   for (int k = threadIdx.x; k < (2 << MB); k += blockDim.x) cl[k] = cons[k];
-  stage_exp_table(etab);
+  if constexpr (ES == 2)
+    stage_exp_table(etab);
+  else
+    stage_exp_table_banked(etab);
   __syncthreads();
+  const lds_exptab et = (lds_exptab)etab + (ES == 2 ? 0 : 2 * (threadIdx.x & 15));
   // grid-stride over the symbols: the LDS staging above is paid once per
   // workgroup, not once per 256 symbols
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < todo; i += (long long)gridDim.x * blockDim.x) {
@@ -69,7 +79,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? K
     double out[MB];
     if constexpr (EXACT) {
       demap_symbol_t<MB, false>((lds_cons)cl, (lds_exptab)etab, yy.x, yy.y, hh.x, hh.y, var, out);
-    } else if (!demap_symbol_t<MB, true>((lds_cons)cl, (lds_exptab)etab, yy.x, yy.y, hh.x, hh.y, var, out)) {
+    } else if (!demap_symbol_t<MB, true, lds_cons, ES>((lds_cons)cl, et, yy.x, yy.y, hh.x, hh.y, var, out)) {
       p0[gid * MB] = -1.0;  // the sentinel (a P0 is in [1e-12, 1 - 1e-12])
       const unsigned k = atomicAdd(d.cnt, 1u);
       if (k < (unsigned)d.cap) d.idx[k] = (int32_t)gid;

@@ -36,6 +36,20 @@ typedef const __attribute__((address_space(3))) uint64_t *lds_exptab;
 __device__ __forceinline__ void stage_exp_table(uint64_t *dst) {  // dst: a __shared__ array
   for (int i = threadIdx.x; i < 256; i += blockDim.x) dst[i] = kExpTabDev[i];
 }
+// Bank-private form (ES = kExpBanked u64 per entry): 16 copies of the table,
+// entry i of copy L at byte 256 i + 16 L, and lane L (mod 16) reads copy L
+// (the base pointer it passes is dst + 2 (lane & 15)).  A ds_read_b128 is
+// serviced 16 lanes per pass, one 4-bank group per lane, so the random table
+// indices of a wave's exps no longer collide on banks (32 KB of LDS; the
+// 64QAM demap_kernel).
+constexpr int kExpBanked = 32;
+__device__ __forceinline__ void stage_exp_table_banked(uint64_t *dst) {  // dst: a __shared__ array of 4096
+  for (int i = threadIdx.x; i < 128 * 16; i += blockDim.x) {
+    const int e = i >> 4, L = i & 15;
+    dst[e * kExpBanked + 2 * L] = kExpTabDev[2 * e];
+    dst[e * kExpBanked + 2 * L + 1] = kExpTabDev[2 * e + 1];
+  }
+}
 
 // glibc's exp (kml_exp_t<true>) on its main path only: exact for x == 0 and
 // for 2^-54 <= |x| < 512, where glibc takes no special case (x == 0 gives
@@ -45,6 +59,7 @@ __device__ __forceinline__ bool exp_core_ok(double x) {
   const double a = fabs(x);  // branch-free: (2^-54 <= |x| < 512) or x == 0
   return ((a >= 0x1p-54) & (a < 512.0)) | (x == 0.0);
 }
+template <int ES = 2>  // u64 per table entry: 2 (stage_exp_table) or kExpBanked
 __device__ __forceinline__ double exp_core(double x, lds_exptab tab) {
   const double InvLn2N = 0x1.71547652b82fep0 * 128;
   const double Shift = 0x1.8p52;
@@ -56,7 +71,7 @@ __device__ __forceinline__ double exp_core(double x, lds_exptab tab) {
   const uint64_t ki = as_u64(kd);
   kd -= Shift;
   const double r = fma(kd, NegLn2loN, fma(kd, NegLn2hiN, x));
-  const int idx = (int)(2 * (ki % 128));
+  const int idx = (int)(ES * (ki % 128));
   const double tail = as_f64(tab[idx]);
   const uint64_t sbits = tab[idx + 1] + (ki << (52 - 7));
   const double r2 = r * r;
@@ -79,7 +94,7 @@ __device__ __forceinline__ double exp_core(double x, lds_exptab tab) {
 //     the check says;
 //   * the weighted sum in [2^-64, 2^64] (it is at least w / KC): the clipped
 //     terms (>= w * 1e-12) and q0, q1 (>= 1e-14, q0 + q1 ~ 2) are inside.
-template <int MB, bool FAST, class CP>
+template <int MB, bool FAST, class CP, int ES = 2>
 __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double yr, double yi, double hr,
                                                double hi, double var, double *out) {
   constexpr int KC = 1 << MB;
@@ -119,7 +134,7 @@ __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double 
     const double x = pr[k] - mx;
     if (FAST) {  // glibc's main path (exp_core), the rest falls back
       eok &= exp_core_ok(x);
-      pr[k] = exp_core(x, etab);
+      pr[k] = exp_core<ES>(x, etab);
     } else {
       pr[k] = kml_exp(x);  // glibc exp, bit-exact (exact_math.hpp)
     }

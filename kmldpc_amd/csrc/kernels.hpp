@@ -37,7 +37,8 @@ struct DevCode {
   const int32_t *pt_vn, *pt_cn, *pt_pos, *pt_vaddr, *pt_xr, *pt_xr_ptr, *pt_xc, *pt_xc_ptr;
   const int32_t *pt_vx, *pt_rx;  // tagged exchange: mailbox index per column edge, per-row (first x, cut mask)
   int pt_G, pt_ncut, pt_mirror;
-  int pt_xr_n[4], pt_xc_n[4];  // exchange-list lengths per member (host copy, launch checks)
+  int pt_pairs;                // every member receives cut-edge messages from every other member
+  int pt_xr_n[8], pt_xc_n[8];  // exchange-list lengths per member (host copy, launch checks)
 };
 
 // Counter block in device memory (uint64):
@@ -118,7 +119,7 @@ hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s);
 int bp_part_group_size(int N, int M, int E, int dv_max, int dc_max, int regular);
 // Does a partition plan (cut edges, most mirror slots of a member, longest
 // exchange list) fit the partitioned kernel's LDS, scratch and tilings?
-bool part_plan_fits(int N, int M, int E, int ncut, int mirror_max, int xmax);
+bool part_plan_fits(int G, int N, int M, int E, int ncut, int mirror_max, int xmax);
 // Name of the cooperative kernel launch_bp_coop runs for this code.
 const char *bp_coop_family(const DevCode &c);
 bool bp_coop_aborted(const BpLaunch &a, int groups, hipStream_t s);

@@ -433,6 +433,14 @@ static bool plan_partition_uncached(const LdpcCode &L, int G, PartitionPlan &out
     return a.R != b.R ? a.R < b.R : a.slot < b.slot;
   });
   out.ncut = (int)cuts.size();
+  {
+    std::vector<char> pair((size_t)G * G, 0);
+    for (const Cut &c : cuts) pair[(size_t)c.R * G + c.S] = 1;
+    out.all_pairs = true;
+    for (int r = 0; r < G; r++)
+      for (int q = 0; q < G; q++)
+        if (r != q && !pair[(size_t)r * G + q]) out.all_pairs = false;
+  }
   if (out.ncut >= (1 << 15)) return false;  // packed (x << 16) entries
   std::vector<std::vector<int32_t>> xr(G), xc(G);
   std::vector<int> mirror_of(cuts.size());

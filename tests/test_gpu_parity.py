@@ -539,16 +539,23 @@ def test_global_slot_cooperative_kernel_still_exact(data_dir, monkeypatch):
         assert r["ret"][i] == ret and np.array_equal(r["cc_hat"][i], cch), i
 
 
+@pytest.mark.parametrize("group", ["8", "4"])
 @pytest.mark.parametrize("tagged", ["1", "0"])
-def test_partitioned_kernel_tagged_exchange_and_deferral(data_dir, monkeypatch, tagged):
-    """bp_part_kernel's tagged exchange (FAST codewords: direct mailbox stores,
-    tag polling, per-iteration early-stop flags) and the barrier-exchange launch
-    it defers the other codewords to: a PEG8064 batch with two codewords outside
-    the fast-division domain (-0.0 / subnormal priors) among FAST ones, iteration
+def test_partitioned_kernel_tagged_exchange_and_deferral(data_dir, monkeypatch, tagged, group):
+    """The partitioned kernels' tagged exchange (FAST codewords: direct mailbox
+    stores, tag polling, per-iteration early-stop flags) — groups of 8 with two
+    codewords in flight per group (bp_part2_kernel, KML_PART_G=8) and groups
+    of 4 with one (KML_PART_G=4) — and the barrier-exchange launch they defer the
+    other codewords to: a PEG8064 batch with two codewords outside the
+    fast-division domain (-0.0 / subnormal priors) among FAST ones, iteration
     budgets 20 and 1, bit-exact against the oracle on ret, cc_hat and the soft
     syndromes; KML_PART_TAGGED=0 (barrier exchange only) gives the same."""
     monkeypatch.setenv("KML_PART_TAGGED", tagged)
-    ctx = ctx_for(data_dir, "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 20)
+    monkeypatch.setenv("KML_PART_G", group)  # fixed when the context builds its partition plan
+    ctx = K.Context(matrix_file=os.path.join(data_dir, "PEG8064regular0.5.txt"),
+                    modem_file=os.path.join(data_dir, "6bits_64QAM_Gray.txt"), is5g=False, active=True,
+                    max_iter=20, device=0)
+    assert ctx.dims["part_group"] == int(group)
     oc = oracle_for(data_dir, "PEG8064regular0.5.txt", False, 20)
     rng = np.random.default_rng(33)
     B = 300
@@ -564,6 +571,7 @@ def test_partitioned_kernel_tagged_exchange_and_deferral(data_dir, monkeypatch, 
             assert np.array_equal(r["uu_hat"][i], uh), (it, i)
             assert np.array_equal(r["cc_hat"][i], cch), (it, i)
             assert np.array_equal(r["syn"][i], syn, equal_nan=True), (it, i)
+    ctx.close()
 
 
 @pytest.mark.parametrize("matrix,modem,is5g,max_iter", CODES)

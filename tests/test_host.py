@@ -31,7 +31,7 @@ def test_library_exports_header_symbols():
     assert len(syms) >= 20
     missing = [s for s in syms if not hasattr(L, s)]
     assert not missing, missing
-    assert L.kml_abi_version() == 1
+    assert L.kml_abi_version() == 2
 
 
 _oracle_codes = {}

@@ -44,6 +44,8 @@ def parse(name):
     """(family, variant) of a rocprofv3 kernel name; variant 'exact' marks a chain's last dispatch."""
     n = name.replace("kml::(anonymous namespace)::", "").replace("void ", "")
     fam = n.split("(")[0].split("<")[0].strip()
+    if fam == "bp_part2_kernel":  # the two-slot tagged launch (groups of 8) of the bp_part_kernel chain
+        return "bp_part_kernel", "fast_tagged"
     if fam not in CHAIN_FAMILIES or "<" not in n:
         return fam, ""
     targs = [t.strip() for t in n.split("<", 1)[1].split(">")[0].split(",")]
