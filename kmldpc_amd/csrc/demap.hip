@@ -35,8 +35,12 @@ namespace {
 // 64QAM: the 64 probabilities of a symbol stay in registers (280 VGPRs
 // unconstrained, one wave per SIMD); KML_DEMAP64_WAVES = 2 caps the kernel at
 // 256 so two waves per SIMD hide the exp table loads and the dependent chains
-#ifndef KML_EXPTAB_BANKED  // (A/B) 0: the 64QAM demap_kernel reads the plain exp table
-#define KML_EXPTAB_BANKED 1
+// (A/B) 1: the 64QAM demap_kernel reads bank-private copies of the exp table
+// (demap_common.hpp stage_exp_table_banked).  Measured: 0.89 ms per 4096
+// PEG8064 codewords against 0.87 with the plain table (profiles/r04_ab2_summary.txt):
+// the bank conflicts were not on the kernel's critical path.
+#ifndef KML_EXPTAB_BANKED
+#define KML_EXPTAB_BANKED 0
 #endif
 #ifndef KML_DEMAP64_WAVES
 #define KML_DEMAP64_WAVES 2
