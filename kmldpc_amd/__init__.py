@@ -30,7 +30,7 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include", "kmldpc_amd.h")
 
 KML_DEVICE_PTRS = 1
 KML_HISTOGRAM = 2
-DIM_NAMES = ["M", "Ncol", "K", "cc_len", "Z", "E", "chk", "max_iter", "bits", "Kc", "S", "bp_lds"]
+DIM_NAMES = ["M", "Ncol", "K", "cc_len", "Z", "E", "chk", "max_iter", "bits", "Kc", "S", "bp_lds", "part_group"]
 
 
 def comm_unique_id():
