@@ -905,6 +905,9 @@ __device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, 
 #ifndef KML_PART_CN_AGE_PRIO
 #define KML_PART_CN_AGE_PRIO 5
 #endif
+#ifndef KML_PART_FLAG_LATE  // (A/B) 0: the last wave of the CN phase posts the flag (returned LDS atomics)
+#define KML_PART_FLAG_LATE 1
+#endif
 #ifndef KML_PART_VN_AGE_PRIO
 #define KML_PART_VN_AGE_PRIO 0
 #endif
@@ -1022,9 +1025,11 @@ __device__ __forceinline__ int part_iterations_tagged(
     int odd, int &iter_out, bool &conv_out, int &pcnt_out, int &decbuf_out, bool sus0 = false) {
   constexpr int DV = 3, DC = 6, H = 3, NW = T / 64;
   const int tid = threadIdx.x;
+#if !KML_PART_FLAG_LATE
   __shared__ int sarrive;  // waves done with the CN phase of this iteration
-  __shared__ int sany;     // bit 0: some member had failing rows after the previous CN phase; bit 1: an unproven quotient
   if (tid == 0) sarrive = 0;
+#endif
+  __shared__ int sany;     // bit 0: some member had failing rows after the previous CN phase; bit 1: an unproven quotient
   int iter = 0, pcnt_prev = 0;
   bool sus = sus0;
   double syn_prev[RC];
@@ -1274,6 +1279,12 @@ __device__ __forceinline__ int part_iterations_tagged(
     pcnt_prev = nfail;  // unsatisfied checks of this iteration's hard decisions (final if the loop ends after it)
     const int wbits = (__ballot(fail) != 0 ? 1 : 0) | (__ballot(sus) != 0 ? 2 : 0);
     KML_STAMP(6);
+#if KML_PART_FLAG_LATE
+    // every wave ORs its bits in (no returned atomic on its path); thread 0
+    // posts the member's flag after the closing barrier below — the partners
+    // read it only after their next VN phase and v2c receive
+    if ((tid & 63) == 0 && wbits) atomicOr(sfail, wbits);
+#else
     if ((tid & 63) == 0) {  // the member's last wave to get here posts its flag
       if (wbits) atomicOr(sfail, wbits);
       if (atomicAdd(&sarrive, 1) == NW - 1) {
@@ -1283,11 +1294,20 @@ __device__ __forceinline__ int part_iterations_tagged(
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+#endif
     KML_STAMP(7);
     // --------------------------------------- receive c2v of the cut edges
     if (iter + 1 < a.iter_count)
       if (!poll_entries<RX, 1>(xc, tb, tb_c2v, smem, tag, abort)) *sdead = 1;
     __syncthreads();
+#if KML_PART_FLAG_LATE
+    if (tid == 0) {
+      const int f = *sfail;
+      *sfail = 0;
+      __hip_atomic_store(&gs->mflag[g & 1][member], ((unsigned long long)(g + 1) << 2) | (unsigned long long)(f & 3),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
     KML_STAMP(8);
     if (*sdead) return -1;
   }
