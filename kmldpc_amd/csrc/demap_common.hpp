@@ -198,70 +198,69 @@ __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double 
 // Hard decisions rr_j = (P0_j > 0.5) of one symbol's MB bits (the metric's
 // kmcodec.cc:111-115) screened in single precision: returns false when some bit
 // is too close to call, and the caller then runs the exact demap_symbol.
-// P0_j > 0.5 iff q0_j > q1_j, where q_b = sum over the points whose label bit j
+// P0_j > 0.5 iff Q0_j > Q1_j, where Q_b = sum over the points whose label bit j
 // is b of c_k = ProbClip(exp(a_k) / sum exp(a)), a_k = dmin - d_k (the common
 // factors w and 1 / sum2 cancel, and ProbClip of the final quotient does not
-// move it across 0.5).  Here a_k is formed in double (d_k = n_k * (1/var),
-// 2^-52 relative), rounded to float (|a_k| <= 40: 2.4e-6 absolute), and
-// exp(a_k) = v_exp_f32(a_k * log2 e) (3.5e-6 absolute in the exponent, 1 ulp);
-// terms with a_k <= -40 are 0 here and below 4.3e-18 exactly, so both clip to
-// 1e-12.  Each c_k is then within 1e-5 relative of the reference's, the
-// sums q within 1.5e-5, and the reference's own rounding is below 1e-13: a bit
-// is decided only when one sum exceeds the other by 2^-12 (2.4e-4) relative.
-// The distances enter only through a_k = dmin - d_k, so the common |y|^2 / var
-// drops out: d_k - |y|^2/var = |c_k|^2 A - 2 Re(c_k B) with A = |h|^2 / var and
-// B = h conj(y) / var, three fp64 operations per point from the staged
-// (|c_k|^2, 2 Re c_k, 2 Im c_k) (scr; the reference's form costs nine).  Their
-// rounding errors are below 2^-50 M, M = max_k (|c_k|^2 |A| + 2 |c_k| |B|) <=
-// 2^20 (checked; beyond it the symbol takes the exact path), i.e. under 1e-9
-// absolute in a_k: far inside the float rounding of a_k the margin covers.
-// (QPSK and 8-point sets keep the direct form: there the setup outweighs the
-// saving, measured 0.96 -> 0.99 ms per 32768 QPSK codewords.)
+// move it across 0.5).  The screen compares instead the unclipped, unnormalised
+// sums q_b = sum of exp(a_k) (one scale factor, sum exp(a), is common to both):
+//   * d_k is formed in double in log2 units, f_k = RN_f32(d_k log2 e), and the
+//     symbol is screened only when fmin = min f_k <= 64; a term that is not
+//     negligible has f_k <= fmin + 58 < 128, so its f_k is within 2^-18 of the
+//     exact value (the double arithmetic adds < 2^-30: the expanded form below
+//     M <= 2^20, checked; the direct form is the reference's own |c_k h - y|^2
+//     times 1 / var log2 e, 2^-51 relative);
+//   * e_k = v_exp_f32(fmin - f_k): the subtraction rounds once (< 2^-19 for
+//     |.| < 64) and v_exp_f32 is within 1 ulp, so e_k = 2^(dmin log2 e - d_k
+//     log2 e + dlt) (1 +- 2^-23) with |dlt| < 2^-17 beyond the error of fmin,
+//     which is a factor common to every term: relative to each other the terms
+//     are within 1e-5, and the float sums add < 65 * 2^-24 relative;
+//   * the clips: ProbClip's floor 1e-12 adds at most 2^6 * 1e-12 to a
+//     normalised Q, and the ceiling 1 only removes rounding; the smaller side of
+//     a decided bit is compared with the larger, which holds at least half of
+//     the total, so both move its ratio by < 1e-9.
+// A bit is decided only when one sum exceeds the other by 2^-12 (2.4e-4)
+// relative, against < 4e-5 of accumulated error (the reference's own rounding
+// is below 1e-13).  Terms with a_k below -88 flush to 0 here and clip to 1e-12
+// there: covered by the clip bound.
+// 16QAM and up: d_k = |c_k|^2 A - 2 Re(c_k B) + |y|^2 / var with A = |h|^2 / var
+// and B = h conj(y) / var, three fmas per point from the staged
+// (|c_k|^2, 2 Re c_k, 2 Im c_k) (scr; the reference's form costs nine);
+// M = cbound (A + |Br| + |Bi|) + |y|^2 / var bounds every partial result.  QPSK
+// and 8-point sets keep the direct form |c_k h - y|^2 / var (there the setup
+// outweighs the saving, measured 0.96 -> 0.99 ms per 32768 QPSK codewords).
 template <int MB, class CP>
 __device__ __forceinline__ bool hard_bits_screen(CP cons, CP scr, double cbound, double yr, double yi, double hr,
                                                  double hi, double inv_var, unsigned &bits) {
   constexpr int KC = 1 << MB;
   constexpr bool kExpand = MB >= 4;
   asm volatile("" : "+v"(scr));  // opaque per call: no hoisting of the point loads out of the caller's loop
-  double A = 0.0, Br = 0.0, Bi = 0.0;
+  const double iv = inv_var * 1.4426950408889634;  // 1 / var in log2 units
+  double A = 0.0, Br = 0.0, Bi = 0.0, Y = 0.0;
   if constexpr (kExpand) {
-    A = (hr * hr + hi * hi) * inv_var;
-    Br = (hr * yr + hi * yi) * inv_var;  // Re(h conj(y)) / var
-    Bi = (hi * yr - hr * yi) * inv_var;  // Im(h conj(y)) / var
-    // cbound >= max(max |c_k|^2, 2 max(|Re c_k|, |Im c_k|)): M <= cbound (A + |Br| + |Bi|)
-    if (!(cbound * (A + fabs(Br) + fabs(Bi)) <= 0x1p20)) return false;
+    A = (hr * hr + hi * hi) * iv;
+    Br = (hr * yr + hi * yi) * iv;  // Re(h conj(y)) / var
+    Bi = (hi * yr - hr * yi) * iv;  // Im(h conj(y)) / var
+    Y = (yr * yr + yi * yi) * iv;
+    // cbound >= max(max |c_k|^2, 2 max(|Re c_k|, |Im c_k|))
+    if (!(cbound * (A + fabs(Br) + fabs(Bi)) + Y <= 0x1p20)) return false;
   }
-  auto dist = [&](int k) {
+  float e[KC];  // f_k, then exp2(fmin - f_k) in place
+  float fmin = INFINITY;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    double d;
     if constexpr (kExpand) {
-      return fma(scr[3 * k], A, -fma(scr[3 * k + 1], Br, -(scr[3 * k + 2] * Bi)));
+      d = fma(scr[3 * k], A, fma(-scr[3 * k + 1], Br, fma(scr[3 * k + 2], Bi, Y)));
     } else {
       const double cr = cons[2 * k], ci = cons[2 * k + 1];
       const double sr = cr * hr - ci * hi - yr;
       const double si = cr * hi + ci * hr - yi;
-      return (sr * sr + si * si) * inv_var;
+      d = (sr * sr + si * si) * iv;
     }
-  };
-  // for large constellations d_k is computed twice (for dmin, then for a_k)
-  // rather than kept: KC doubles would cost 2 KC registers
-  constexpr bool kRecompute = KC >= 32;
-  double dk[kRecompute ? 1 : KC];
-  double dmin = 0.0;
-#pragma unroll
-  for (int k = 0; k < KC; ++k) {
-    const double d = dist(k);
-    if (!kRecompute) dk[k] = d;
-    dmin = k == 0 ? d : fmin(dmin, d);
+    e[k] = (float)d;
+    fmin = fminf(fmin, e[k]);
   }
-  if (kRecompute) asm volatile("" : "+v"(scr), "+v"(cons));  // reload the points (no CSE across the passes)
-  float e[KC];
-  float sum = 0.f;
-#pragma unroll
-  for (int k = 0; k < KC; ++k) {
-    const float a = (float)(dmin - (kRecompute ? dist(k) : dk[k]));
-    e[k] = a > -40.f ? __builtin_amdgcn_exp2f(a * 1.44269504f) : 0.f;
-    sum += e[k];
-  }
-  const float inv = 1.f / sum;
+  if (!(fmin <= 64.f)) return false;  // (NaN too)
   float q0[MB], q1[MB];
 #pragma unroll
   for (int j = 0; j < MB; ++j) q0[j] = q1[j] = 0.f;
@@ -277,7 +276,7 @@ __device__ __forceinline__ bool hard_bits_screen(CP cons, CP scr, double cbound,
   float tot = 0.f;
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
-    const float c = fminf(fmaxf(e[k] * inv, 1e-12f), 1.f);
+    const float c = __builtin_amdgcn_exp2f(fmin - e[k]);
     if (kComplement) tot += c;
 #pragma unroll
     for (int j = 0; j < MB; ++j) {
