@@ -101,28 +101,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? K
 // demapper decides: the FAST one (EXACT = false), which leaves the codeword to
 // the EXACT kernel when it cannot prove a symbol (returns false, nothing
 // written), or the exact one.
+// 64QAM: the undecided (candidate, symbol) pairs are listed in LDS (up to
+// kRescanCap; past it the second pass scans every pair for the mark), so the
+// exact demapper runs on a dense list — one pass for the ~0.25 % undecided
+// pairs of a codeword instead of one per wave-iteration that holds one.
+constexpr int kRescanCap = 256;
 template <int MB, bool EXACT>
 __device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const double2 *__restrict__ y, int S,
                                                const double2 *__restrict__ h4, int nc, double var, double inv_var,
                                                double *__restrict__ metrics, int32_t *__restrict__ chosen,
                                                unsigned char *smem, lds_cons cl, lds_exptab etab, lds_cons scr,
                                                double scb) {
-  int *cnt = reinterpret_cast<int *>(smem);  // 4 counters, the undecided flag, the unproven flag
+  int *cnt = reinterpret_cast<int *>(smem);  // 4 counters, the undecided count, the unproven flag
   unsigned char *hb = smem + 32;             // [4][cc_len]
+  int *und = reinterpret_cast<int *>(smem + 32 + ((4 * (size_t)c.cc_len + 3) & ~(size_t)3));  // [kRescanCap]
   constexpr bool kRescan = MB >= 5;
   const int tid = threadIdx.x;
   if (tid < 6) cnt[tid] = 0;
   __syncthreads();
   const double2 *yy = y + (long long)cw * S;
-  for (int i = tid; i < nc * S; i += blockDim.x) {
-    const int q = i / S, j = i - q * S;
+  // (candidate q, symbol j) of pair i = q S + j, advanced without a division
+  int q = tid / S, j = tid - q * S;
+  for (int i = tid; i < nc * S; i += blockDim.x, j += blockDim.x) {
+    while (j >= S) {
+      j -= S;
+      ++q;
+    }
     const double2 v = yy[j];
     const double2 hh = h4[(long long)cw * nc + q];
     unsigned bits;
     if (!hard_bits_screen<MB>(cl, scr, scb, v.x, v.y, hh.x, hh.y, inv_var, bits)) {
       if (kRescan) {
         hb[q * c.cc_len + j * MB] = 2;  // undecided: the demap pass below
-        cnt[4] = 1;
+        const int u = atomicAdd(&cnt[4], 1);
+        if (u < kRescanCap) und[u] = i;
         continue;
       }
       double out[MB];
@@ -142,7 +154,10 @@ __device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const d
   __syncthreads();
   if (kRescan && cnt[4]) {  // 64QAM: the demapper in a pass of its own keeps its
                             // registers out of the screening loop's
-    for (int i = tid; i < nc * S; i += blockDim.x) {
+    const int nu = cnt[4];
+    const bool listed = nu <= kRescanCap;
+    for (int u = tid; u < (listed ? nu : nc * S); u += blockDim.x) {
+      const int i = listed ? und[u] : u;
       const int q = i / S, j = i - q * S;
       if (hb[q * c.cc_len + j * MB] != 2) continue;
       const double2 v = yy[j];
@@ -369,7 +384,7 @@ hipError_t launch_cand_metric(const DevCode &c, int bits, const double *cons, co
   if (B == 0) return hipSuccess;
   if (nc < 1 || nc > 4) return hipErrorInvalidValue;
   if (!d.idx || !d.cnt || d.cap < B) return hipErrorInvalidValue;  // every codeword may defer
-  const size_t lds = 32 + 4 * (size_t)c.cc_len;
+  const size_t lds = 32 + ((4 * (size_t)c.cc_len + 3) & ~(size_t)3) + (bits >= 5 ? 4 * (size_t)kRescanCap : 0);
   int dev = 0, ncu = 0;
   hipGetDevice(&dev);
   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
