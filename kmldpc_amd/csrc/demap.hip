@@ -113,7 +113,7 @@ __device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const d
                                                unsigned char *smem, lds_cons cl, lds_exptab etab, lds_cons scr,
                                                double scb) {
   int *cnt = reinterpret_cast<int *>(smem);  // 4 counters, the undecided count, the unproven flag
-  unsigned char *hb = smem + 32;             // [4][cc_len]
+  unsigned char *hb = smem + 32;             // [cc_len][4]: column-major, a row's parity of all candidates in one word
   int *und = reinterpret_cast<int *>(smem + 32 + ((4 * (size_t)c.cc_len + 3) & ~(size_t)3));  // [kRescanCap]
   constexpr bool kRescan = MB >= 5;
   const int tid = threadIdx.x;
@@ -132,7 +132,7 @@ __device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const d
     unsigned bits;
     if (!hard_bits_screen<MB>(cl, scr, scb, v.x, v.y, hh.x, hh.y, inv_var, bits)) {
       if (kRescan) {
-        hb[q * c.cc_len + j * MB] = 2;  // undecided: the demap pass below
+        hb[(j * MB) * 4 + q] = 2;  // undecided: the demap pass below
         const int u = atomicAdd(&cnt[4], 1);
         if (u < kRescanCap) und[u] = i;
         continue;
@@ -149,7 +149,7 @@ __device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const d
       for (int b = 0; b < MB; ++b) bits |= (out[b] > 0.5 ? 1u : 0u) << b;  // kmcodec.cc:111-115
     }
 #pragma unroll
-    for (int b = 0; b < MB; ++b) hb[q * c.cc_len + j * MB + b] = (bits >> b) & 1;
+    for (int b = 0; b < MB; ++b) hb[(j * MB + b) * 4 + q] = (bits >> b) & 1;
   }
   __syncthreads();
   if (kRescan && cnt[4]) {  // 64QAM: the demapper in a pass of its own keeps its
@@ -159,7 +159,7 @@ __device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const d
     for (int u = tid; u < (listed ? nu : nc * S); u += blockDim.x) {
       const int i = listed ? und[u] : u;
       const int q = i / S, j = i - q * S;
-      if (hb[q * c.cc_len + j * MB] != 2) continue;
+      if (hb[(j * MB) * 4 + q] != 2) continue;
       const double2 v = yy[j];
       const double2 hh = h4[(long long)cw * nc + q];
       double out[MB];
@@ -170,22 +170,17 @@ __device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const d
         continue;
       }
 #pragma unroll
-      for (int b = 0; b < MB; ++b) hb[q * c.cc_len + j * MB + b] = out[b] > 0.5 ? 1 : 0;  // kmcodec.cc:111-115
+      for (int b = 0; b < MB; ++b) hb[(j * MB + b) * 4 + q] = out[b] > 0.5 ? 1 : 0;  // kmcodec.cc:111-115
     }
   }
   __syncthreads();
   if (!EXACT && cnt[5]) return false;  // uniform: every thread read the flag after the barrier
   int local[4] = {0, 0, 0, 0};
   for (int r = tid; r < c.M; r += blockDim.x) {
-    int p[4] = {0, 0, 0, 0};
-    for (int e = c.row_ptr[r]; e < c.row_ptr[r + 1]; ++e) {
-      const int col = c.row_col[e];
+    unsigned p = 0;  // byte q: candidate q's parity (bytes of candidates >= nc unused)
+    for (int e = c.row_ptr[r]; e < c.row_ptr[r + 1]; ++e) p ^= *reinterpret_cast<const unsigned *>(hb + 4 * c.row_col[e]);
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (q < nc) p[q] ^= hb[q * c.cc_len + col];
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) local[q] += p[q];
+    for (int q = 0; q < 4; ++q) local[q] += (p >> (8 * q)) & 1;
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -206,7 +201,19 @@ __device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const d
 // FAST: one workgroup per codeword, unproven codewords onto the defer list
 // (at most B entries: d.cap >= B).  EXACT: the listed codewords, grid-stride.
 template <int MB, bool EXACT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? 3 : 1))) void cand_metric_kernel(
+// Minimum waves per SIMD of the metric kernel: <= 4-point sets 8 (64 VGPRs;
+// 10 spilled, on the inline demap of undecided symbols only): QPSK 0.79 -> 0.66
+// ms per 32768 codewords against the unconstrained 88 VGPRs / 5 waves (6 waves:
+// 0.73; profiles/r04_ab9_summary.txt); 64QAM 4 (128 VGPRs: the 64 screen terms
+// fit, the spills sit in the undecided list's exact demap): 0.73 -> 0.70 ms per
+// 4096 PEG8064 codewords against 3 (r04_ab10_summary.txt).
+#ifndef KML_CM_SMALL_WAVES
+#define KML_CM_SMALL_WAVES 8
+#endif
+#ifndef KML_CM_BIG_WAVES
+#define KML_CM_BIG_WAVES 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? KML_CM_BIG_WAVES : MB <= 2 ? KML_CM_SMALL_WAVES : 1))) void cand_metric_kernel(
     DevCode c, const double *__restrict__ cons, const double2 *__restrict__ y, int S, const double2 *__restrict__ h4,
     int nc, double var, double inv_var, double *__restrict__ metrics, int32_t *__restrict__ chosen, DemapDefer d) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
