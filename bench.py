@@ -49,8 +49,8 @@ KERNEL_NOTES = {
     "bp_regular_kernel": "sum-product BP, messages LDS-resident",
     "bp_irregular_kernel": "sum-product BP, irregular degrees, messages LDS-resident",
     "bp_coop_kernel": "sum-product BP, 4 workgroups per codeword, messages in L2",
-    "bp_part_kernel": "sum-product BP, partitioned LDS slots + cut-edge mailboxes: 8 workgroups per codeword, two "
-                      "codewords in flight per group (bp_part2_kernel)",
+    "bp_part_kernel": "sum-product BP, partitioned LDS slots + cut-edge mailboxes: 4 workgroups on one XCD per "
+                      "codeword, tagged mailbox exchange",
     "bp_kernel": "sum-product BP, generic",
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
@@ -586,6 +586,11 @@ def main():
     if os.environ.get("KML_DUMP_MAPS"):  # diagnostics: map a crash at exit to its library
         with open("/proc/self/maps") as src, open(os.environ["KML_DUMP_MAPS"], "w") as dst:
             dst.write(src.read())
+    if os.environ.get("KML_EXIT_RESET") == "1":  # diagnostics (W3): tear the device down before exit()
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")  # the library's runtime (torch's is never started here)
+        print("hipDeviceSynchronize:", hip.hipDeviceSynchronize(), "hipDeviceReset:", hip.hipDeviceReset(),
+              file=sys.stderr, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
