@@ -501,9 +501,11 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
         const double2 v = yy[j];
         double out[DMB];
         if constexpr (EXACT)
-          demap_symbol_t<DMB, false>((lds_cons)dcons, (lds_exptab)detab, v.x, v.y, hh.x, hh.y, a.sym_var, out);
+          demap_symbol_t<DMB, false, lds_cons, 2, false>((lds_cons)dcons, (lds_exptab)detab, v.x, v.y, hh.x, hh.y,
+                                                          a.sym_var, out);
         else  // no exact fallback in the FAST kernel (its registers): a failing symbol defers the codeword
-          dok &= demap_symbol_t<DMB, true>((lds_cons)dcons, (lds_exptab)detab, v.x, v.y, hh.x, hh.y, a.sym_var, out);
+          dok &= demap_symbol_t<DMB, true, lds_cons, 2, false>((lds_cons)dcons, (lds_exptab)detab, v.x, v.y, hh.x,
+                                                              hh.y, a.sym_var, out);
 #pragma unroll
         for (int b = 0; b < DMB; ++b) p0s[j * DMB + b] = out[b];
       }
