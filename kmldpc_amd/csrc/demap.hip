@@ -33,8 +33,8 @@ namespace {
 // EXACT: the listed symbols on the exact path (div_rn, kml_exp), or, when the
 // list overflowed, every symbol carrying the sentinel.
 // 64QAM: the 64 probabilities of a symbol stay in registers (280 VGPRs
-// unconstrained, one wave per SIMD); KML_DEMAP64_WAVES = 2 caps the kernel at
-// 256 so two waves per SIMD hide the exp table loads and the dependent chains
+// unconstrained, one wave per SIMD); KML_DEMAP64_WAVES caps the kernel so that
+// several waves per SIMD hide the exp table loads and the dependent chains
 // (A/B) 1: the 64QAM demap_kernel reads bank-private copies of the exp table
 // (demap_common.hpp stage_exp_table_banked).  Measured: 0.89 ms per 4096
 // PEG8064 codewords against 0.87 with the plain table (profiles/r04_ab2_summary.txt):
@@ -42,11 +42,17 @@ namespace {
 #ifndef KML_EXPTAB_BANKED
 #define KML_EXPTAB_BANKED 0
 #endif
+// Round 4: 64QAM at 3 waves per SIMD (168 VGPRs: 37 spilled, as many as at
+// 256), 16QAM at 4 (128 VGPRs, 2 spilled): 0.87 -> 0.84 ms and 0.295 -> 0.291
+// ms per 4096 PEG8064 / 16384 BG2 codewords (profiles/r04_ab17_summary.txt)
 #ifndef KML_DEMAP64_WAVES
-#define KML_DEMAP64_WAVES 2
+#define KML_DEMAP64_WAVES 3
+#endif
+#ifndef KML_DEMAP16_WAVES
+#define KML_DEMAP16_WAVES 4
 #endif
 template <int MB, bool EXACT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? KML_DEMAP64_WAVES : 1))) void demap_kernel(const double *__restrict__ cons, const double2 *__restrict__ y,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? KML_DEMAP64_WAVES : MB == 4 ? KML_DEMAP16_WAVES : 1))) void demap_kernel(const double *__restrict__ cons, const double2 *__restrict__ y,
                                                     int S, int reps, const double2 *__restrict__ h, int h_stride,
                                                     const int32_t *__restrict__ h_sel, double var, int B,
                                                     double *__restrict__ p0, DemapDefer d) {
