@@ -87,7 +87,7 @@ enum {
   KML_DIM_KC = 9,       /* constellation points */
   KML_DIM_S = 10,       /* symbols per codeword */
   KML_DIM_BP_LDS = 11,  /* 1 if the decoder keeps messages in LDS */
-  KML_DIM_PART_G = 12,  /* workgroups per codeword of the partitioned decoder (8 or 4), 0 when not used */
+  KML_DIM_PART_G = 12,  /* workgroups per codeword of the partitioned decoder (4), 0 when not used */
   KML_DIM_COUNT = 13
 };
 

@@ -61,13 +61,10 @@ struct GroupSync {
   unsigned long long mflag[2][8];
 };
 
-// Workgroups per codeword of the partitioned kernels: 8 (the two-slot tagged
-// kernel bp_part2_kernel, and its barrier / exact follow-up launches) or 4
-// (KML_PART_G=4: the one-slot tagged kernel of round 3).
-constexpr int kP2G = 8;
-#ifndef KML_PART_G_DEFAULT  // workgroups per codeword of the partitioned decoder (4: one-slot kernel, 8: two slots)
-#define KML_PART_G_DEFAULT 4
-#endif
+// Workgroups per codeword of the partitioned kernel.  (Groups of 8 with two
+// codewords in flight, and two 512-thread workgroups per CU, measured slower
+// in round 4 and were removed: DESIGN.md, Round-4 changes.)
+constexpr int kPartG = 4;
 
 // c2v placement: a c2v message lives in the lower or upper 8 bytes of its
 // 16-byte slot (the v2c pair fills the whole slot), by bit 2 of its row's
@@ -113,64 +110,14 @@ __host__ __device__ constexpr bool part_tagged_fits(int E, int ncut) {
   return 6LL * ncut + 2 <= 2LL * E && 24LL * ncut <= 16LL * kMbOob;
 }
 // The partitioned launches' scratch per group (double2): the barrier-exchange
-// mailboxes (3 ncut doubles) and the one-slot kernel's tagged ones in E
-// double2, the two-slot kernel's two tagged mailboxes (48 ncut bytes) in
-// 3 ncut + 8; the tagged launch's defer list follows the groups' strides.
-__host__ __device__ constexpr long long part_group_stride_n(int E, int ncut) {
-  return ((E > 3LL * ncut + 8 ? (long long)E : 3LL * ncut + 8) + 7) & ~7LL;
-}
-__host__ __device__ inline long long part_group_stride(const DevCode &c) { return part_group_stride_n(c.E, c.pt_ncut); }
-// The two-slot kernel: one column and one half-row per lane (T = 1024), the
-// row owner's v2c entry offsets and the column's out-of-range kMbOob within 32
-// bits, a nonempty cut.
-constexpr bool part2_fits(int N, int M, int ncut) {
-  return ncut > 0 && 24LL * ncut <= 16LL * kMbOob && N / kP2G <= 1024 && 2 * (M / kP2G) <= 1024;
-}
-inline bool part2_usable(const DevCode &c) { return c.pt_G == kP2G && c.pt_pairs && part2_fits(c.N, c.M, c.pt_ncut); }
+// mailboxes (3 ncut doubles) and the tagged ones, in E double2; the tagged
+// launch's defer list follows the groups' strides.
+__host__ __device__ inline long long part_group_stride(const DevCode &c) { return ((long long)c.E + 7) & ~7LL; }
 // byte offset of the deferred-codeword count in the sync block (past the abort word)
 constexpr size_t part_defer_offset(int groups) { return sizeof(GroupSync) * (size_t)groups + 16; }
-// byte offset of the two-slot kernel's Part2Sync blocks (past the defer count)
-constexpr size_t part2_sync_offset(int groups) { return (part_defer_offset(groups) + 16 + 63) & ~(size_t)63; }
 
 __device__ __forceinline__ unsigned ld_rlx(const unsigned *p) {  // L1-bypassing (sc1) load
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Group barrier.  Returns false when the launch is aborted (a poll timed out).
-// same_xcd: members share an L2, plain stores + vmcnt(0) suffice; otherwise
-// agent-scope release / acquire fences (L2 write-back / L1 invalidate).
-template <int kG>
-__device__ __forceinline__ bool group_barrier(GroupSync *gs, unsigned &gen, bool same_xcd, unsigned *abort) {
-  if (same_xcd)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else
-    __threadfence();
-  __syncthreads();
-  gen += kG;
-  __shared__ int ok;
-  if (threadIdx.x == 0) {
-    if (!same_xcd) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __hip_atomic_fetch_add(&gs->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int good = 1;
-    for (long long spin = 0; ld_rlx(&gs->bar) < gen; ++spin) {
-      if (spin > kSpinLimit || ld_rlx(abort)) {
-        __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        good = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (!same_xcd) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    ok = good;
-  }
-  __syncthreads();
-  return ok != 0;
 }
 
 // loads of data other members wrote: bypass the vector L1
@@ -191,358 +138,6 @@ __device__ __forceinline__ double swap_pair(double x) {
   return __hiloint2double(hi2, lo2);
 }
 __device__ __forceinline__ int swap_pair_i(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }
-
-// Per-launch control block shared by every workgroup.
-struct CoopCtl {
-  unsigned abort;  // a group barrier timed out: every workgroup exits
-};
-
-// Returns -1 when the launch aborts, 1 when a FAST decode met a quotient
-// dd_check could not prove (exact_div.hpp; the caller redoes the codeword with
-// FAST = false), 0 when done.
-template <int kG, int RV, int RC, bool SYN, bool FAST>
-__device__ __forceinline__ int coop_iterations(const DevCode &c, const BpLaunch &a, int cw, GroupSync *gs,
-                                                unsigned &gen, bool same_xcd, unsigned *abort, double2 *slots,
-                                                uint8_t *gc, const int (&vpos)[RV], const int (&es)[RV][3],
-                                                const bool (&vact)[RV], const double (&pv)[RV], const int (&crow)[RC],
-                                                const int (&cbase)[RC], const int (&ccol)[RC][3],
-                                                const bool (&cact)[RC], int odd, int member, int &iter_out,
-                                                bool &conv_out, bool sus0 = false) {
-  constexpr int DV = 3, DC = 6, H = 3;
-  int iter = 0;
-  bool conv = false, sus = sus0;
-  for (; iter < a.iter_count; ++iter) {
-    // ------------------------------------------------------------ VN phase
-    // falling wave priorities within a phase (see bp_regular.hip)
-    __builtin_amdgcn_s_setprio(3);
-    {
-      double c0s[RV][DV];
-#pragma unroll
-      for (int r = 0; r < RV; ++r)
-#pragma unroll
-        for (int k = 0; k < DV; ++k) c0s[r][k] = ld_nt(&slots[es[r][k]].x);
-      // one column's chains at a time (column-major): the FAST divisions'
-      // proofs keep a normalisation's operands live, and interleaving the RV
-      // columns step by step doubled the live set (scratch spills in the loop)
-#pragma unroll
-      for (int r = 0; r < RV; ++r) {
-        double a0 = pv[r], a1 = 1.0 - pv[r], al0[DV], al1[DV];
-#pragma unroll
-        for (int k = 0; k < DV; ++k) {
-          al0[k] = a0;
-          al1[k] = a1;
-          const double c0 = c0s[r][k];
-          const double n0 = a0 * c0;
-          const double n1 = a1 * (1.0 - c0);
-          if (k + 1 < DV) {
-            div2<FAST>(n0, n1, n0 + n1, a0, a1, sus);
-          } else {
-            const int hd = hard_decision<FAST>(n0, n1, sus);
-            if (vact[r]) gc[vpos[r]] = (unsigned char)hd;
-          }
-        }
-        if (r == RV / 2) __builtin_amdgcn_s_setprio(1);  // falling priorities within the phase
-        double b0 = 1.0, b1 = 1.0;
-#pragma unroll
-        for (int k = DV - 1; k >= 0; --k) {
-          const bool unit = FAST && k == DV - 1;
-          const double t0 = unit ? al0[k] : al0[k] * b0;
-          const double t1 = unit ? al1[k] : al1[k] * b1;
-          double q0, q1;
-          if (unit)  // beta = (1, 1): t is the normalised alpha, its sum within ulps of 1 (bp_common.hpp rcp_near1)
-            div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
-          else
-            div2<FAST>(t0, t1, t0 + t1, q0, q1, sus);
-          if (vact[r]) slots[es[r][k]] = make_double2(q0, q1);
-          if (k > 0) {
-            const double c0 = c0s[r][k];
-            if (unit) {  // (c0, 1 - c0) / (c0 + (1 - c0)): the sum rounds to exactly 1 (bp_common.hpp)
-              b0 = c0;
-              b1 = 1.0 - c0;
-            } else {
-              div2<FAST>(b0 * c0, b1 * (1.0 - c0), b0 * c0 + b1 * (1.0 - c0), b0, b1, sus);
-            }
-          }
-        }
-      }
-      __builtin_amdgcn_s_setprio(0);
-    }
-    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return -1;
-
-    // -------------------- early-stop parity check, folded into the CN barrier
-    // Every member ORs its failing-row flag now and runs the CN phase
-    // speculatively; the flag is read after the CN barrier.  A converged
-    // codeword's speculative CN results (slots) are never read again, and its
-    // syndromes are only written when the phase counts.
-    {
-      int fail = 0;
-#pragma unroll
-      for (int r = 0; r < RC; ++r) {
-        int p = 0;
-#pragma unroll
-        for (int k = 0; k < H; ++k) p ^= ld_nt(&gc[ccol[r][k]]);
-        fail |= cact[r] ? (p ^ swap_pair_i(p)) : 0;
-      }
-      const unsigned bits = (__ballot(fail) != 0 ? 1u : 0u) | (__ballot(sus) != 0 ? 2u : 0u);
-      if (bits && (threadIdx.x & 63) == 0)
-        __hip_atomic_fetch_or(&gs->flag[iter & 1], bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-
-    // ------------------------------------------------------------ CN phase
-    // Step st: loads first, the c2v of this step from the swapped states, the
-    // chain update (which waits for the loads), and only then the c2v stores:
-    // the partner lane's load of the slot stored here has completed by then.
-    double syn0[RC];
-    {
-      double x0[RC][H], x1[RC][H];
-      double s0[RC], s1[RC];
-#pragma unroll
-      for (int r = 0; r < RC; ++r) {
-        s0[r] = 1.0;
-        s1[r] = 0.0;
-      }
-      __builtin_amdgcn_s_setprio(2);
-#pragma unroll
-      for (int st = 0; st < DC; ++st) {
-        if (st == 2) __builtin_amdgcn_s_setprio(1);
-        if (st == 4) __builtin_amdgcn_s_setprio(0);
-        const bool advance = SYN || st + 1 < DC;
-        double m0[RC], m1[RC];
-        if (advance) {
-#pragma unroll
-          for (int r = 0; r < RC; ++r) {
-            const double2 m = ld_nt(&slots[cbase[r] + (odd ? DC - 1 - st : st)]);
-            m0[r] = m.x;
-            m1[r] = m.y;
-          }
-        }
-        double q[RC];
-#pragma unroll
-        for (int r = 0; r < RC; ++r) {
-          q[r] = 0.0;
-          if (st < H) {
-            x0[r][st] = s0[r];
-            x1[r][st] = s1[r];
-          } else {
-            const double y0 = swap_pair(s0[r]);
-            const double y1 = swap_pair(s1[r]);
-            const double o0 = x0[r][DC - 1 - st], o1 = x1[r][DC - 1 - st];
-            const bool unit = FAST && st == DC - 1;
-            const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
-            const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
-            q[r] = clip_c2v<FAST>(div1<FAST, true>(t0, t0 + t1));
-          }
-        }
-        if (advance) {
-#pragma unroll
-          for (int r = 0; r < RC; ++r) {
-            const bool unit = FAST && st == 0;
-            const double n0 = unit ? m0[r] : s0[r] * m0[r] + s1[r] * m1[r];
-            const double n1 = unit ? m1[r] : s0[r] * m1[r] + s1[r] * m0[r];
-            div2<FAST, true>(n0, n1, n0 + n1, s0[r], s1[r], sus);
-          }
-        }
-        if (st >= H) {
-#pragma unroll
-          for (int r = 0; r < RC; ++r)
-            if (cact[r]) slots[cbase[r] + (odd ? st : DC - 1 - st)].x = q[r];
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < RC; ++r) syn0[r] = s0[r];
-    }
-    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return -1;
-    const unsigned fl = ld_rlx(&gs->flag[iter & 1]);
-    if (FAST && (fl & 2u)) {  // an unproven quotient in this VN phase (every member reads the same word)
-      iter_out = iter;
-      conv_out = false;
-      return 1;
-    }
-    if (!(fl & 1u)) {  // every row satisfied: stop before this CN phase
-      conv = true;
-      break;
-    }
-    if (member == 0 && threadIdx.x == 0)  // cleared before anyone can OR into it (next VN barrier)
-      __hip_atomic_store(&gs->flag[(iter + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if constexpr (SYN) {
-#pragma unroll
-      for (int r = 0; r < RC; ++r)
-        if (cact[r] && !odd) a.syn[(long long)cw * c.M + crow[r]] = syn0[r];  // alpha past the last edge (:274)
-    }
-  }
-  iter_out = iter;
-  conv_out = conv;
-  return 0;
-}
-
-// EXACT = false: the FAST kernel (defers non-FAST and suspect codewords to
-// a.defer_idx); EXACT = true: the exact path over a defer list (bp_regular.hip).
-template <int kG, int T, int RV, int RC, bool SYN, bool EXACT>
-__global__ __launch_bounds__(T) void bp_coop_kernel(DevCode c, BpLaunch a, GroupSync *gsync, uint8_t *gcch,
-                                                    unsigned *abort, unsigned int *queue, int fast_allowed) {
-  const double plo = fast_prior_lo(c.dv_max);  // FAST prior domain (bp_common.hpp)
-  const int tid = threadIdx.x;
-  const int odd = tid & 1;
-  const int member = (blockIdx.x >> 3) % kG;
-  const int group = (blockIdx.x / (8 * kG)) * 8 + (blockIdx.x & 7);
-  GroupSync *gs = gsync + group;
-  double2 *slots = a.gslots + (size_t)group * c.E;
-  uint8_t *gc = gcch + (size_t)group * c.N;
-
-  // static assignment: member m owns vn positions [v_lo, v_hi) and rows [r_lo, r_hi);
-  // every index the iterations use is register-resident
-  const int v_lo = (int)((long long)c.N * member / kG), v_hi = (int)((long long)c.N * (member + 1) / kG);
-  const int r_lo = (int)((long long)c.M * member / kG), r_hi = (int)((long long)c.M * (member + 1) / kG);
-  int vpos[RV], vcol[RV], es[RV][3];
-  bool vact[RV];
-#pragma unroll
-  for (int r = 0; r < RV; ++r) {
-    const int p = v_lo + r * T + tid;
-    vact[r] = p < v_hi;
-    vpos[r] = vact[r] ? p : v_lo;
-    vcol[r] = c.vn_order[vpos[r]];
-    const int b = c.col_ptr[vcol[r]];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) es[r][k] = c.col_slot[b + k];
-  }
-  int crow[RC], cbase[RC], ccol[RC][3];
-  bool cact[RC];
-#pragma unroll
-  for (int r = 0; r < RC; ++r) {
-    const int q = r_lo + ((r * T + tid) >> 1);  // lane pairs share a row
-    cact[r] = q < r_hi;
-    crow[r] = c.cn_order[cact[r] ? q : r_lo];
-    cbase[r] = c.row_ptr[crow[r]];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) ccol[r][k] = c.reg_pos[c.row_col[cbase[r] + (odd ? 3 + k : k)]];
-  }
-
-  // do the group's members share an XCD (one L2)?  HW_REG_XCC_ID, bits [3:0]
-  unsigned gen = 0;
-  if (a.B_dev && *a.B_dev == 0) return;  // an empty defer list: every workgroup leaves before the first barrier
-  const int B = a.B_dev ? (int)*a.B_dev : a.B;
-  if (tid == 0) {
-    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
-    __hip_atomic_fetch_or(&gs->xcc, 1u << xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (!group_barrier<kG>(gs, gen, false, abort)) return;
-  const bool same_xcd = __popc(ld_rlx(&gs->xcc)) == 1;
-
-  for (;;) {
-    if (member == 0 && tid == 0) {
-      __hip_atomic_store(&gs->cw, atomicAdd(queue, 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&gs->nofast, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&gs->errs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&gs->pcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&gs->flag[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&gs->flag[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return;
-    const int entry = (int)ld_rlx(&gs->cw);
-    if (entry >= B) break;
-    const int cw = a.cw_idx ? a.cw_idx[entry] : entry;
-    const double *p0 = a.p0 + (long long)cw * a.p0_stride;
-    if (a.p0_sel) p0 += (long long)a.p0_sel[cw] * a.p0_sel_stride;
-
-    double pv[RV];
-    bool ok = true;
-#pragma unroll
-    for (int r = 0; r < RV; ++r) {
-      pv[r] = (vcol[r] >= c.punct) ? p0[vcol[r] - c.punct] : 0.5;
-      ok = ok && fast_prior_ok(pv[r], plo);
-    }
-    // InitMsg on this member's share of the slots
-    {
-      const int e_lo = (int)((long long)c.E * member / kG), e_hi = (int)((long long)c.E * (member + 1) / kG);
-      for (int e = e_lo + tid; e < e_hi; e += T) slots[e].x = 0.5;
-    }
-    if (__ballot(!ok) != 0 && (tid & 63) == 0)
-      __hip_atomic_fetch_or(&gs->nofast, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return;
-    const bool fast = (fast_allowed & 1) && !ld_rlx(&gs->nofast);
-
-    int iter = 0;
-    bool conv = false;
-    if constexpr (!EXACT) {
-      int st = 1;  // 1: to the exact kernel
-      if (fast)
-        st = coop_iterations<kG, RV, RC, SYN, true>(c, a, cw, gs, gen, same_xcd, abort, slots, gc, vpos, es, vact, pv,
-                                                    crow, cbase, ccol, cact, odd, member, iter, conv,
-                                                    (fast_allowed & 2) != 0);
-      if (st < 0) return;
-      if (st == 1) {  // every member took this branch (the flag word / nofast are group-wide)
-        if (member == 0 && tid == 0) {
-          a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = cw;
-          if (fast && a.counters) atomicAdd(&a.counters[CNT_REDONE], 1ull);
-        }
-        continue;
-      }
-    } else {
-      if (coop_iterations<kG, RV, RC, SYN, false>(c, a, cw, gs, gen, same_xcd, abort, slots, gc, vpos, es, vact, pv,
-                                                  crow, cbase, ccol, cact, odd, member, iter, conv) < 0)
-        return;
-    }
-
-    // ---- outputs: every member writes its share; member 0 the scalars
-    if (a.iter_count > 0) {
-      if (a.uu_hat) {
-        uint8_t *u = a.uu_hat + (long long)cw * c.K;
-        const int lo = (int)((long long)c.K * member / kG), hi = (int)((long long)c.K * (member + 1) / kG);
-        for (int i = lo + tid; i < hi; i += T) u[i] = ld_nt(&gc[c.reg_pos[i + c.info_off]]);
-      }
-      if (a.cc_hat) {
-        uint8_t *o = a.cc_hat + (long long)cw * c.N;
-        for (int v = v_lo + tid; v < v_hi; v += T) o[c.vn_order[v]] = ld_nt(&gc[v]);
-      }
-      if (a.parity_cnt) {
-        int cnt = 0;
-#pragma unroll
-        for (int r = 0; r < RC; ++r) {
-          int p = 0;
-#pragma unroll
-          for (int k = 0; k < 3; ++k) p ^= ld_nt(&gc[ccol[r][k]]);
-          const int full = p ^ swap_pair_i(p);
-          if (!odd && cact[r]) cnt += full;
-        }
-        if (cnt) __hip_atomic_fetch_add(&gs->pcnt, (unsigned)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (a.ref_bits) {
-        const uint64_t *ref = a.ref_bits + (long long)cw * c.Kw;
-        const int lo = (int)((long long)c.Kw * member / kG), hi = (int)((long long)c.Kw * (member + 1) / kG);
-        int errs = 0;
-        for (int w = lo + tid; w < hi; w += T) {
-          uint64_t word = 0;
-          const int base = w * 64;
-          const int nb = min(64, c.K - base);
-          for (int j = 0; j < nb; ++j) word |= (uint64_t)ld_nt(&gc[c.reg_pos[c.info_off + base + j]]) << j;
-          errs += __popcll(word ^ ref[w]);
-        }
-        if (errs) __hip_atomic_fetch_add(&gs->errs, (unsigned)errs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if (!group_barrier<kG>(gs, gen, same_xcd, abort)) return;  // the members' sums are complete
-    if (member == 0 && tid == 0) {
-      const int errs = (int)ld_rlx(&gs->errs);
-      const int pcnt = (int)ld_rlx(&gs->pcnt);
-      if (a.ret) a.ret[cw] = iter + (iter < a.max_iter);
-      if (a.iters) a.iters[cw] = iter;
-      if (a.parity_cnt) a.parity_cnt[cw] = a.iter_count > 0 ? pcnt : 0;
-      if (a.cw_err && a.ref_bits) a.cw_err[cw] = a.iter_count > 0 ? errs : 0;
-      if (a.counters) {
-        const unsigned long long vn = conv ? (unsigned long long)iter + 1 : (unsigned long long)iter;
-        atomicAdd(&a.counters[CNT_VN_PHASES], vn);
-        atomicAdd(&a.counters[CNT_CN_PHASES], (unsigned long long)iter);
-        if (conv) atomicAdd(&a.counters[CNT_CONVERGED], 1ull);
-        if (a.ref_bits && a.iter_count > 0) {
-          atomicAdd(&a.counters[CNT_ERR_BIT], (unsigned long long)errs);
-          atomicAdd(&a.counters[CNT_ERR_BLK], errs > 0 ? 1ull : 0ull);
-          atomicAdd(&a.counters[CNT_TOT_BIT], (unsigned long long)c.K);
-          atomicAdd(&a.counters[CNT_TOT_BLK], 1ull);
-        }
-      }
-    }
-  }
-}
 
 #ifdef KML_STAMPS
 // Phase timing of the partitioned kernel (a KML_STAMPS=1 build only): wave 0
@@ -1326,7 +921,7 @@ __device__ __forceinline__ int part_iterations_tagged(
 // kernel over what remains.  Each follow-up launch is usually empty.
 template <int kG, int T, int RV, int RC, int RX, bool SYN, bool TAGGED, bool EXACT>
 // (groups of 8 at T = 512: two workgroups per CU, <= 128 VGPRs; KML_PART_MODE=2wg)
-__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(kG == 8 && T == 512 ? 4 : 1))) void bp_part_kernel(DevCode c, BpLaunch a, GroupSync *gsync, uint8_t *gcch,
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_part_kernel(DevCode c, BpLaunch a, GroupSync *gsync, uint8_t *gcch,
                                                     unsigned *abort, unsigned int *queue, int fast_allowed) {
   const double plo = fast_prior_lo(c.dv_max);  // FAST prior domain (bp_common.hpp)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1581,528 +1176,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(kG == 8 && T 
   }
 }
 
-// ===========================================================================
-// bp_part2_kernel: the partitioned decoder with TWO codewords in flight per
-// group (PEG8064; groups of kP2G = 8 workgroups on one XCD, one per CU).
-//
-// Why.  The one-slot tagged kernel (above) spends ~40% of an iteration
-// waiting: after its VN phase a member polls the cut-edge v2c its partners
-// have just written, after its CN phase the c2v (the L2 hand-off latency plus
-// the members' skew; profiles/r04_ab1_part_stamps_branchfree.txt).  Nothing of
-// the same codeword can fill that wait: 89% of the rows have a cut edge.  A
-// second codeword can.  Each member holds an eighth of TWO codewords (2 x 48 KB
-// of row slots instead of 1 x 97 KB) and runs
-//     VN(A) VN(B) | barrier | CN(A) CN(B) | barrier | ...
-// so between a slot's send and its receive there is a whole phase of the
-// other slot's work.
-//
-// Exchange (the tagged protocol of part_iterations_tagged, per slot): every
-// cut edge has a v2c entry (16 B) and a c2v entry (8 B) per slot; the
-// producer writes it straight from the arithmetic with a tag, the consumer
-// polls its own entries — the column owner's lane its column's c2v (into
-// registers), the row owner's lane pair its row's v2c (into the row slots,
-// read by the same wave) — so no barrier follows a receive.  v2c words carry
-// bit 63 = counter & 1 (bit 62 of the first word is the column's decision),
-// c2v words bits 63:62 = counter & 3.  A slot's counter g runs on across its
-// codewords, and a stop skips at most one counter value (the CN phase of the
-// iteration after the one that converged), so the stalest c2v entry a poll
-// can meet is two counter values old and no flush is needed at a stop; a v2c
-// entry is rewritten at every counter value.  The one-slot kernel's
-// ordering arguments hold per slot (every member receives v2c from every
-// other member: PartitionPlan::all_pairs).
-//
-// Early stop, one phase late as in the one-slot kernel: after the CN phases
-// each wave ORs its failing-row bit into an LDS word per slot; after the
-// closing barrier wave 0 posts the member's flag; after the next VN phases
-// and barrier every wave polls the 8 members' flags itself.
-//
-// Codeword hand-over without group barriers: member 0 publishes each slot's
-// codeword k + 1 when the slot starts codeword k (next[slot][(k + 1) & 1]);
-// the members' per-codeword sums (error bits, unsatisfied checks) meet in one
-// 64-bit atomic per slot and codeword (acc[slot][k & 1]), whose last adder
-// writes the codeword's outputs and counters.  Codewords whose priors are not
-// FAST (part2_screen_kernel), or every codeword under KML_FORCE_REDO or when
-// the group does not share one XCD, go to the barrier-exchange launch.
-constexpr int kP2T = 1024;
-constexpr int kP2Dummy = 64;  // per slot: the dummy slots of the lanes' branch-free stores (cut / inactive)
-
-struct Part2Sync {
-  unsigned xcc, bar;
-  unsigned long long mflag[2][2][kP2G];  // [slot][counter & 1][member]: ((counter + 1) << 2) | failing rows
-  unsigned long long next[2][2];          // [slot][k & 1]: ((k + 1) << 32) | queue entry of the slot's k-th codeword
-  unsigned long long acc[2][2];           // [slot][k & 1]: errs << 40 | unsatisfied checks << 16 | members done
-};
-
-__host__ __device__ constexpr int part2_slot_bytes(int M) { return (M / kP2G * 6 + kP2Dummy) * 16; }
-size_t part2_lds_bytes(const DevCode &c) { return 2 * (size_t)part2_slot_bytes(c.M) + 4 * (size_t)(c.N / kP2G); }
-
-// Poll up to 3 c2v entries (byte offsets off[k], need bit k) until their tags
-// (bits 63:62) read tag2; the values, tags stripped, go to v[k].  pre: the
-// words of a first poll issued earlier (the caller's prefetch).
-__device__ __forceinline__ bool p2_poll_c2v(__amdgpu_buffer_rsrc_t mb, const unsigned (&off)[3], unsigned need,
-                                            unsigned tag2, double (&v)[3], unsigned *abort,
-                                            const unsigned long long (&pre)[3]) {
-  for (long long spin = 0; need; ++spin) {
-    unsigned long long w[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) w[k] = spin == 0 ? pre[k] : (need >> k) & 1 ? mb_ld64(mb, off[k]) : 0ull;
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-      if (((need >> k) & 1) && (hi_of(w[k]) >> 30) == tag2) {
-        v[k] = __longlong_as_double((long long)(w[k] & 0x3FFFFFFFFFFFFFFFull));
-        need &= ~(1u << k);
-      }
-    if (need && (spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
-      __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-  }
-  return true;
-}
-
-// Poll up to 3 v2c entries (16 B) until both words' bit 63 read tag; each is
-// stored, bit 63 cleared (the decision bit 62 kept), to the LDS slot lds[k].
-__device__ __forceinline__ bool p2_poll_v2c(__amdgpu_buffer_rsrc_t mb, const unsigned (&off)[3],
-                                            const unsigned (&lds)[3], unsigned need, unsigned tag,
-                                            unsigned char *sbase, unsigned *abort, const u32x4 (&pre)[3]) {
-  for (long long spin = 0; need; ++spin) {
-    u32x4 w[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-      if (spin == 0)
-        w[k] = pre[k];
-      else if ((need >> k) & 1)
-        w[k] = __builtin_amdgcn_raw_buffer_load_b128(mb, (int)off[k], 0, kAuxSc1);
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-      if (((need >> k) & 1) && (w[k].y >> 31) == tag && (w[k].w >> 31) == tag) {
-        u32x4 x = w[k];
-        x.y &= 0x7FFFFFFFu;
-        x.w &= 0x7FFFFFFFu;
-        *reinterpret_cast<u32x4 *>(sbase + lds[k]) = x;
-        need &= ~(1u << k);
-      }
-    if (need && (spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
-      __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-  }
-  return true;
-}
-
-// Poll a 64-bit word until its high half reads want (bounded; false: abort).
-__device__ __forceinline__ bool p2_wait_hi(const unsigned long long *p, unsigned want, unsigned long long &v,
-                                           unsigned *abort) {
-  for (long long spin = 0;; ++spin) {
-    v = ld_rlx64(p);
-    if ((unsigned)(v >> 32) == want) return true;
-    if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
-      __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// Poll a member's early-stop flag word until it holds counter want - 1's post
-// ((want) << 2 | bits).
-__device__ __forceinline__ bool p2_wait_flag(const unsigned long long *p, unsigned want, unsigned long long &v,
-                                             unsigned *abort, unsigned long long pre) {
-  for (long long spin = 0;; ++spin) {
-    v = spin == 0 ? pre : ld_rlx64(p);
-    if ((v >> 2) == (unsigned long long)want) return true;
-    if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
-      __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-  }
-}
-
-// Member 0's dequeue: the next FAST entry (the others go to the barrier-
-// exchange launch's list: bit 31 = the exact launch), or an entry >= B.
-__device__ __forceinline__ int p2_dequeue(const BpLaunch &a, int B, const uint8_t *elig, unsigned *queue) {
-  for (;;) {
-    const int e = (int)atomicAdd(queue, 1u);
-    if (e >= B || elig[e]) return e;
-    const int raw = a.cw_idx ? a.cw_idx[e] : e;
-    a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = (int)((unsigned)raw | 0x80000000u);
-  }
-}
-
-template <bool SYN>
-__global__ __launch_bounds__(kP2T) void bp_part2_kernel(DevCode c, BpLaunch a, Part2Sync *psync, unsigned *abort,
-                                                        unsigned int *queue, const uint8_t *elig, int mode) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int DV = 3, DC = 6, H = 3;
-  const int tid = threadIdx.x, lane = tid & 63, odd = tid & 1;
-  const int member = (blockIdx.x >> 3) % kP2G;
-  const int group = (blockIdx.x / (8 * kP2G)) * 8 + (blockIdx.x & 7);
-  Part2Sync *ps = psync + group;
-  const int MG = c.M / kP2G, NG = c.N / kP2G, EG = MG * DC;
-  const int SB = part2_slot_bytes(c.M);
-  uint8_t *decs = smem + 2 * SB;  // [slot][counter & 1][NG] decisions
-  const int ncut = c.pt_ncut;
-  char *mb0 = reinterpret_cast<char *>(a.gslots + (size_t)group * (size_t)part_group_stride(c));
-  const __amdgpu_buffer_rsrc_t rsv[2] = {mailbox_rsrc(mb0, 24 * ncut), mailbox_rsrc(mb0 + 24 * ncut, 24 * ncut)};
-  const unsigned c2v0 = 16u * (unsigned)ncut;  // each slot's c2v entries follow its v2c entries
-
-  // ---- the lane's column (VN) and half-row (CN): the same in both slots
-  const int vp = member * NG + tid;
-  const bool vact = tid < NG;
-  const int vcol = vact ? c.pt_vn[vp] : 0;
-  unsigned ve[DV];    // (v2c entry, or kMbOob) << 17 | (2 LDS slot + c2v half), slot-relative; cut and
-                      // inactive edges point at the lane's dummy slot
-  unsigned cmask = 0; // bit k: edge k is cut (its c2v is polled)
-  unsigned coff[DV];  // c2v entry offsets of the cut edges
-#pragma unroll
-  for (int k = 0; k < DV; ++k) {
-    const int vx = vact ? c.pt_vx[vp * DV + k] : -1;
-    const int sl = vact && vx < 0 ? c.pt_vaddr[vp * DV + k] >> 4 : EG + lane;
-    const int half = sl < EG ? ((sl / DC) >> 2) & 1 : 1;
-    ve[k] = ((unsigned)(vx >= 0 ? vx : kMbOob) << 17) | (unsigned)(2 * sl + half);
-    if (vx >= 0) cmask |= 1u << k;
-    coff[k] = c2v0 + 8u * (unsigned)(vx >= 0 ? vx : 0);
-  }
-  const int li = tid >> 1;
-  const bool cact = li < MG;
-  const int cli = cact ? li : 0;
-  const int crow = c.pt_cn[member * MG + cli];
-  const int cbase = cli * DC * 16;
-  const unsigned crx = cact ? (unsigned)c.pt_rx[member * MG + cli] : 0u;  // (first x << 8) | cut mask by row position
-  const int cwb = cact ? cbase + ((cli >> 2) & 1) * 8 : EG * 16;       // c2v write base (inactive: the dummy slots)
-  unsigned rneed = 0, roff[H], rlds[H];  // my half-row's cut v2c entries and their row slots
-#pragma unroll
-  for (int k = 0; k < H; ++k) {
-    const unsigned e = odd ? H + k : k;
-    const unsigned x = __popc(crx & 0x3Fu & ((1u << e) - 1u)) + (crx >> 8);
-    if ((crx >> e) & 1) rneed |= 1u << k;
-    roff[k] = x * 16u;
-    rlds[k] = (unsigned)(cbase + (int)e * 16);
-  }
-
-  __shared__ int sflag[2];  // per slot: failing rows after this round's CN phase (some wave)
-  __shared__ int sacc[2];   // per slot: the epilogue's error bits << 16 | unsatisfied checks
-  if (tid < 2) {
-    sflag[tid] = 0;
-    sacc[tid] = 0;
-  }
-
-  // ---- start: the members meet once (an arrival counter), XCD bits
-  if (tid == 0) {
-    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
-    __hip_atomic_fetch_or(&ps->xcc, 1u << xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(&ps->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (tid < 64) {
-    bool ok = true;
-    if (tid == 0)
-      for (long long spin = 0; ld_rlx(&ps->bar) < (unsigned)kP2G; ++spin)
-        if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
-          __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok = false;
-          break;
-        }
-    if (__ballot(!ok)) return;  // wave 0 leaves; the barrier below waits for the surviving waves only
-  }
-  __syncthreads();
-  const bool same_xcd = __popc(ld_rlx(&ps->xcc)) == 1;
-  const int B = a.B_dev ? (int)*a.B_dev : a.B;
-  // mode bit 0: FAST allowed, bit 1: KML_FORCE_REDO.  Not FAST-only (or across
-  // XCDs): member 0 hands every entry to the barrier-exchange launches.
-  if (!same_xcd || (mode & 3) != 1) {
-    if (member == 0 && tid == 0)
-      for (int e; (e = (int)atomicAdd(queue, 1u)) < B;) {
-        const int raw = a.cw_idx ? a.cw_idx[e] : e;
-        a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = (mode & 1) && elig[e] ? raw : (int)((unsigned)raw | 0x80000000u);
-      }
-    return;
-  }
-  if (member == 0 && tid == 0)  // each slot's first codeword
-    for (int s = 0; s < 2; ++s)
-      __hip_atomic_store(&ps->next[s][0], (1ull << 32) | (unsigned)p2_dequeue(a, B, elig, queue), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-
-  int entry[2], cw[2] = {0, 0}, it[2] = {0, 0}, k[2] = {0, 0}, nfail[2] = {0, 0};
-  unsigned g[2] = {0, 0};
-  double pv[2] = {0.5, 0.5}, syn_prev[2] = {0.0, 0.0};
-  // the slot's k-th codeword (every wave polls the published entry itself);
-  // member 0 then publishes the slot's next one.  false: abort.
-  auto start = [&](int s) -> bool {
-    int e = 0;
-    bool ok = true;
-    if (lane == 0) {
-      unsigned long long v = 0;
-      ok = p2_wait_hi(&ps->next[s][k[s] & 1], (unsigned)(k[s] + 1), v, abort);
-      e = (int)(unsigned)v;
-    }
-    if (__ballot(!ok)) return false;
-    e = __builtin_amdgcn_readfirstlane(__shfl(e, 0));
-    if (member == 0 && tid == 0 && e < B)
-      __hip_atomic_store(&ps->next[s][(k[s] + 1) & 1],
-                         ((unsigned long long)(unsigned)(k[s] + 2) << 32) | (unsigned)p2_dequeue(a, B, elig, queue),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    entry[s] = e < B ? e : -1;
-    it[s] = 0;
-    nfail[s] = 0;
-    syn_prev[s] = 0.0;
-    if (e < B) {
-      cw[s] = (a.cw_idx ? a.cw_idx[e] : e) & 0x7FFFFFFF;
-      const double *p0 = a.p0 + (long long)cw[s] * a.p0_stride;
-      if (a.p0_sel) p0 += (long long)a.p0_sel[cw[s]] * a.p0_sel_stride;
-      pv[s] = vact && vcol >= c.punct ? p0[vcol - c.punct] : 0.5;
-    }
-    return true;
-  };
-  if (!start(0) || !start(1)) return;
-
-  // ---- VN phase of slot s, iteration it[s], counter g[s]
-  auto vn = [&](int s, const unsigned long long (&cpre)[DV]) -> bool {
-    unsigned char *sb = smem + s * SB;
-    const unsigned tag = g[s] & 1u;
-    double c0c[DV];
-    if (it[s] == 0) {  // InitMsg (binaryldpccodec.cc:166-170): every c2v is 0.5
-#pragma unroll
-      for (int k2 = 0; k2 < DV; ++k2) c0c[k2] = 0.5;
-    } else {
-#pragma unroll
-      for (int k2 = 0; k2 < DV; ++k2) c0c[k2] = *reinterpret_cast<const double *>(sb + vaddr_c2v((int)ve[k2]));
-      double pc[DV] = {0.0, 0.0, 0.0};
-      if (!p2_poll_c2v(rsv[s], coff, cmask, (g[s] - 1u) & 3u, pc, abort, cpre)) return false;
-#pragma unroll
-      for (int k2 = 0; k2 < DV; ++k2)
-        if ((cmask >> k2) & 1) c0c[k2] = pc[k2];
-    }
-    __builtin_amdgcn_s_setprio(3);
-    double a0 = pv[s], a1 = 1.0 - pv[s], al0[DV], al1[DV];
-    unsigned hdb = 0;
-    bool sus = false;
-#pragma unroll
-    for (int k2 = 0; k2 < DV; ++k2) {
-      al0[k2] = a0;
-      al1[k2] = a1;
-      const double c0 = c0c[k2];
-      const double n0 = a0 * c0;
-      const double n1 = a1 * (1.0 - c0);
-      if (k2 + 1 < DV) {
-        div2<true>(n0, n1, n0 + n1, a0, a1, sus);
-      } else {
-        const int hd = hard_decision<true>(n0, n1, sus);
-        hdb = hd ? kHdHi : 0u;
-        if (vact) decs[(s * 2 + (int)(it[s] & 1)) * NG + tid] = (unsigned char)hd;
-      }
-    }
-    __builtin_amdgcn_s_setprio(1);
-    double b0 = 1.0, b1 = 1.0;
-#pragma unroll
-    for (int k2 = DV - 1; k2 >= 0; --k2) {
-      const bool unit = k2 == DV - 1;
-      const double t0 = unit ? al0[k2] : al0[k2] * b0;
-      const double t1 = unit ? al1[k2] : al1[k2] * b1;
-      double q0, q1;
-      if (unit)
-        div2<true, true>(t0, t1, t0 + t1, q0, q1, sus);
-      else
-        div2<true>(t0, t1, t0 + t1, q0, q1, sus);
-      {  // branch-free: the v2c entry (out of range for a local edge) and the LDS slot (the dummy for a cut edge)
-        const unsigned va = ve[k2];
-        const unsigned tb_tag = tag ? kTagHi : 0u;
-        mb_st128(rsv[s], (va >> 17) << 4, or_hi(q0, tb_tag | hdb), or_hi(q1, tb_tag));
-        *reinterpret_cast<double2 *>(sb + vaddr_slot((int)va)) = make_double2(or_hi(q0, hdb), q1);
-      }
-      if (k2 > 0) {
-        const double c0 = c0c[k2];
-        if (unit) {
-          b0 = c0;
-          b1 = 1.0 - c0;
-        } else {
-          div2<true>(b0 * c0, b1 * (1.0 - c0), b0 * c0 + b1 * (1.0 - c0), b0, b1, sus);
-        }
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    return true;
-  };
-
-  // ---- CN phase of slot s (+ the parity check of VN it[s]'s decisions)
-  auto cn = [&](int s, const u32x4 (&vpre)[H]) -> bool {
-    unsigned char *sb = smem + s * SB;
-    const unsigned tag = g[s] & 1u;
-    if (!p2_poll_v2c(rsv[s], roff, rlds, rneed, tag, sb, abort, vpre)) return false;
-    int par = 0;
-    double x0[H], x1[H], s0 = 1.0, s1 = 0.0;
-    __builtin_amdgcn_s_setprio(2);
-#pragma unroll
-    for (int st = 0; st < DC; ++st) {
-      if (st == 4) __builtin_amdgcn_s_setprio(0);
-      const bool advance = SYN || st + 1 < DC || st < H;
-      double m0 = 0.0, m1 = 0.0;
-      if (advance) {
-        const double2 m = *reinterpret_cast<const double2 *>(sb + cbase + (odd ? DC - 1 - st : st) * 16);
-        if (st < H) par ^= (__double2hiint(m.x) >> 30) & 1;
-        m0 = and_hi(m.x, ~kHdHi);
-        m1 = m.y;
-      }
-      if (st < H) {
-        x0[st] = s0;
-        x1[st] = s1;
-      } else {
-        const double y0 = swap_pair(s0);
-        const double y1 = swap_pair(s1);
-        const double o0 = x0[DC - 1 - st], o1 = x1[DC - 1 - st];
-        const bool unit = st == DC - 1;
-        const double t0 = unit ? y0 : o0 * y0 + o1 * y1;
-        const double t1 = unit ? y1 : o0 * y1 + o1 * y0;
-        const double q = clip_c2v<true>(div1<true, true>(t0, t0 + t1));
-        // branch-free: the c2v entry of a cut edge (out of range otherwise) and the row slot's c2v half
-        const unsigned e = odd ? st : DC - 1 - st;
-        const unsigned cut = __builtin_amdgcn_ubfe(crx, e, 1);
-        const unsigned x = __popc(__builtin_amdgcn_ubfe(crx, 0, e)) + (crx >> 8);
-        mb_st64(rsv[s], cut ? c2v0 + x * 8u : kMbOobOff, or_hi(q, (g[s] & 3u) << 30));
-        *reinterpret_cast<double *>(sb + cwb + (int)e * 16) = q;
-      }
-      if (st + 1 < DC || SYN) {
-        const bool unit = st == 0;
-        const double n0 = unit ? m0 : s0 * m0 + s1 * m1;
-        const double n1 = unit ? m1 : s0 * m1 + s1 * m0;
-        bool sus = false;
-        div2<true, true>(n0, n1, n0 + n1, s0, s1, sus);
-      }
-    }
-    syn_prev[s] = s0;
-    const int full = par ^ swap_pair_i(par);
-    nfail[s] = (cact && !odd) ? full : 0;
-    const bool fail = cact && full;
-    if (__ballot(fail) != 0 && lane == 0) atomicOr(&sflag[s], 1);
-    return true;
-  };
-
-  // ---- a slot's codeword ends after iteration `iter` (conv: its checks held)
-  auto finish = [&](int s, int iter, bool conv) {
-    const int decbuf = conv ? (iter & 1) : ((iter - 1) & 1);
-    const int pc = conv ? 0 : nfail[s];
-    int err = 0;
-    if (vact && a.iter_count > 0) {
-      const int hd = decs[(s * 2 + decbuf) * NG + tid];
-      if (a.cc_hat) a.cc_hat[(long long)cw[s] * c.N + vcol] = (uint8_t)hd;
-      const int i = vcol - c.info_off;
-      if (i >= 0 && i < c.K) {
-        if (a.uu_hat) a.uu_hat[(long long)cw[s] * c.K + i] = (uint8_t)hd;
-        if (a.ref_bits) err = (int)((a.ref_bits[(long long)cw[s] * c.Kw + (i >> 6)] >> (i & 63)) & 1ull) != hd;
-      }
-    }
-    if (err | pc) atomicAdd(&sacc[s], (err << 16) + pc);
-    __syncthreads();
-    if (tid == 0) {
-      const int v = sacc[s];
-      sacc[s] = 0;
-      const unsigned long long add = ((unsigned long long)(unsigned)(v >> 16) << 40) |
-                                     ((unsigned long long)(unsigned)(v & 0xFFFF) << 16) | 1ull;
-      const unsigned long long old =
-          __hip_atomic_fetch_add(&ps->acc[s][k[s] & 1], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((old & 0xFFFF) == (unsigned long long)(kP2G - 1)) {  // the last member: the codeword's totals
-        const unsigned long long tot = old + add;
-        __hip_atomic_store(&ps->acc[s][k[s] & 1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int errs = (int)(tot >> 40), pcnt = (int)((tot >> 16) & 0xFFFFFF);
-        const int c_ = cw[s];
-        if (a.ret) a.ret[c_] = iter + (iter < a.max_iter);
-        if (a.iters) a.iters[c_] = iter;
-        if (a.parity_cnt) a.parity_cnt[c_] = a.iter_count > 0 ? pcnt : 0;
-        if (a.cw_err && a.ref_bits) a.cw_err[c_] = a.iter_count > 0 ? errs : 0;
-        if (a.counters) {
-          atomicAdd(&a.counters[CNT_VN_PHASES], conv ? (unsigned long long)iter + 1 : (unsigned long long)iter);
-          atomicAdd(&a.counters[CNT_CN_PHASES], (unsigned long long)iter);
-          if (conv) atomicAdd(&a.counters[CNT_CONVERGED], 1ull);
-          if (a.ref_bits && a.iter_count > 0) {
-            atomicAdd(&a.counters[CNT_ERR_BIT], (unsigned long long)errs);
-            atomicAdd(&a.counters[CNT_ERR_BLK], errs > 0 ? 1ull : 0ull);
-            atomicAdd(&a.counters[CNT_TOT_BIT], (unsigned long long)c.K);
-            atomicAdd(&a.counters[CNT_TOT_BLK], 1ull);
-          }
-        }
-      }
-    }
-    ++k[s];
-  };
-
-  for (;;) {
-    if (entry[0] < 0 && entry[1] < 0) break;
-    // Every receive is issued one phase ahead (its first poll's words are
-    // prefetched): the c2v of both slots (the partners' CN phases of the
-    // previous round) before the VN phases, the v2c and the early-stop flags of
-    // both slots before the CN phases, so a poll's L2 round trip overlaps the
-    // other slot's arithmetic instead of stalling every wave at once.
-    unsigned long long cpre[2][DV];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int k2 = 0; k2 < DV; ++k2)
-        cpre[s][k2] = entry[s] >= 0 && it[s] > 0 && it[s] < a.iter_count && ((cmask >> k2) & 1)
-                          ? mb_ld64(rsv[s], coff[k2])
-                          : 0ull;
-    // VN phases of both slots (a slot past its last iteration skips it)
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-      if (entry[s] >= 0 && it[s] < a.iter_count)
-        if (!vn(s, cpre[s])) return;
-    __syncthreads();
-    unsigned long long fpre[2];
-    u32x4 vpre[2][H];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      fpre[s] = entry[s] >= 0 && it[s] > 0 && lane < kP2G ? ld_rlx64(&ps->mflag[s][(g[s] - 1u) & 1][lane]) : 0ull;
-#pragma unroll
-      for (int k2 = 0; k2 < H; ++k2)
-        vpre[s][k2] = entry[s] >= 0 && it[s] < a.iter_count && ((rneed >> k2) & 1)
-                          ? __builtin_amdgcn_raw_buffer_load_b128(rsv[s], (int)roff[k2], 0, kAuxSc1)
-                          : u32x4{0u, 0u, 0u, 0u};
-    }
-    // the early-stop decisions, then the CN phases
-    bool ran[2] = {false, false};
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      if (entry[s] < 0) continue;
-      const int i = it[s];
-      bool stop = false, conv = false;
-      int iter = i;
-      if (i > 0) {  // the members' flags after CN i - 1 (counter g - 1): every wave polls them
-        unsigned long long v = 0;
-        bool ok = true;
-        if (lane < kP2G) ok = p2_wait_flag(&ps->mflag[s][(g[s] - 1u) & 1][lane], g[s], v, abort, fpre[s]);
-        if (__ballot(!ok)) return;
-        if (__ballot(lane < kP2G && (v & 1) != 0) == 0) {  // every row held after VN i - 1: the reference stops there
-          stop = conv = true;
-          iter = i - 1;
-          if (i < a.iter_count) ++g[s];  // VN i ran: the next codeword starts one counter later
-        } else if constexpr (SYN) {  // CN i - 1 counted: its syndromes stand (alpha past the last edge, :274)
-          if (cact && !odd) a.syn[(long long)cw[s] * c.M + crow] = syn_prev[s];
-        }
-      }
-      if (!stop && i >= a.iter_count) stop = true;  // the iteration budget is spent
-      if (stop) {
-        finish(s, iter, conv);
-        if (!start(s)) return;
-        continue;
-      }
-      if (!cn(s, vpre[s])) return;
-      ran[s] = true;
-    }
-    __syncthreads();
-    // post the flags of the CN phases just run (wave 0, lane = slot); advance their slots
-    if (tid < 2 && ran[tid]) {
-      const int f = sflag[tid];
-      sflag[tid] = 0;
-      __hip_atomic_store(&ps->mflag[tid][g[tid] & 1][member], ((unsigned long long)(g[tid] + 1u) << 2) | (unsigned)f,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-      if (ran[s]) {
-        ++g[s];
-        ++it[s];
-      }
-  }
-}
-
 // Launch of a grid whose workgroups must all be co-resident (the group
 // barriers and tag polls wait on each other): a cooperative launch, which
 // also keeps another process's kernels from taking CUs the grid needs (two
@@ -2150,91 +1223,6 @@ hipError_t launch_part_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int
   return launch_resident((const void *)kern, (unsigned)(groups * kG), (unsigned)T, args, (unsigned)lds, s);
 }
 
-// Which codewords the two-slot kernel may take: every prior in the FAST domain
-// (bp_common.hpp fast_prior_ok) — the one-slot kernel's per-codeword check,
-// decided before the launch so that no member waits on the others' verdict.
-__global__ __launch_bounds__(256) void part2_screen_kernel(DevCode c, BpLaunch a, int B, uint8_t *elig) {
-  const int e = blockIdx.x;
-  if (e >= B) return;
-  const int raw = a.cw_idx ? a.cw_idx[e] : e;
-  const int cw = raw & 0x7FFFFFFF;
-  const double *p0 = a.p0 + (long long)cw * a.p0_stride;
-  if (a.p0_sel) p0 += (long long)a.p0_sel[cw] * a.p0_sel_stride;
-  const double plo = fast_prior_lo(c.dv_max);
-  bool ok = true;
-  for (int j = c.punct + (int)threadIdx.x; j < c.N; j += blockDim.x) ok = ok && fast_prior_ok(p0[j - c.punct], plo);
-  const int all = __syncthreads_and(ok ? 1 : 0);
-  if (threadIdx.x == 0) elig[e] = (raw >= 0 && all) ? 1 : 0;
-}
-
-// The two-slot tagged launch (bp_part2_kernel) of launch_part_chain.  d: the
-// batch, with the tagged launch's defer list (the barrier-exchange launch's
-// entries).
-template <bool SYN>
-hipError_t launch_part2_t(const DevCode &c, const BpLaunch &d, hipStream_t s, int fast, int groups, bool reset_abort) {
-  auto kern = bp_part2_kernel<SYN>;
-  const size_t lds = part2_lds_bytes(c);
-  hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(d.queue, 0, sizeof(unsigned int), s);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(d.gsync, 0, sizeof(GroupSync) * (size_t)groups + (reset_abort ? sizeof(unsigned) : 0), s);
-  if (e != hipSuccess) return e;
-  Part2Sync *ps = reinterpret_cast<Part2Sync *>(reinterpret_cast<char *>(d.gsync) + part2_sync_offset(groups));
-  e = hipMemsetAsync(ps, 0, sizeof(Part2Sync) * (size_t)groups, s);
-  if (e != hipSuccess) return e;
-  // every tagged mailbox word starts with all tag bits 1 (counter 0 writes 0)
-  e = hipMemsetAsync(d.gslots, 0xFF, sizeof(double2) * (size_t)groups * (size_t)part_group_stride(c), s);
-  if (e != hipSuccess) return e;
-  uint8_t *elig = reinterpret_cast<uint8_t *>(d.defer_idx + d.B);
-  hipLaunchKernelGGL(part2_screen_kernel, dim3(d.B), dim3(256), 0, s, c, d, d.B, elig);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  DevCode cc = c;
-  BpLaunch aa = d;
-  unsigned *abort = reinterpret_cast<unsigned *>(reinterpret_cast<GroupSync *>(d.gsync) + groups);
-  unsigned int *q = d.queue;
-  const uint8_t *el = elig;
-  int mode = fast & 3;
-  void *args[] = {&cc, &aa, &ps, &abort, &q, &el, &mode};
-  return launch_resident((const void *)kern, (unsigned)(groups * kP2G), (unsigned)kP2T, args, (unsigned)lds, s);
-}
-
-template <int kG, int T, int RV, int RC, bool SYN, bool EXACT>
-hipError_t launch_coop_one(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast, int groups) {
-  auto kern = bp_coop_kernel<kG, T, RV, RC, SYN, EXACT>;
-  hipError_t e = hipMemsetAsync(a.queue, 0, sizeof(unsigned int), s);
-  if (e != hipSuccess) return e;
-  // group blocks, and the abort word unless an unchecked earlier launch may have set it
-  e = hipMemsetAsync(a.gsync, 0, sizeof(GroupSync) * (size_t)groups + (a.reset_abort ? sizeof(unsigned) : 0), s);
-  if (e != hipSuccess) return e;
-  DevCode cc = c;
-  BpLaunch aa = a;
-  GroupSync *gs = reinterpret_cast<GroupSync *>(a.gsync);
-  uint8_t *gcch = a.gcch;
-  unsigned *abort = reinterpret_cast<unsigned *>(gs + groups);
-  unsigned int *q = a.queue;
-  int f = fast;
-  void *args[] = {&cc, &aa, &gs, &gcch, &abort, &q, &f};
-  return launch_resident((const void *)kern, (unsigned)(groups * kG), (unsigned)T, args, 0u, s);
-}
-
-// FAST kernel, then the exact kernel over its defer list (bp_regular.hip launch_reg_t)
-template <int kG, int T, int RV, int RC, bool SYN>
-hipError_t launch_coop_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast, int groups) {
-  if (!(fast & 1)) return launch_coop_one<kG, T, RV, RC, SYN, true>(c, a, s, 0, groups);
-  if (!a.defer_idx || !a.defer_cnt) return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(a.defer_cnt, 0, sizeof(unsigned), s);
-  if (e != hipSuccess) return e;
-  e = launch_coop_one<kG, T, RV, RC, SYN, false>(c, a, s, fast, groups);
-  if (e != hipSuccess) return e;
-  BpLaunch b = a;
-  b.cw_idx = a.defer_idx;
-  b.B_dev = a.defer_cnt;
-  b.reset_abort = false;  // an abort of the FAST launch stays visible
-  return launch_coop_one<kG, T, RV, RC, SYN, true>(c, b, s, 0, groups);
-}
-
 // The partitioned kernel's launches for one batch.  a.defer_* (the caller's
 // list) receives the codewords for the exact launch; d.defer_* (scratch past
 // the groups' mailboxes) the tagged launch's deferrals.
@@ -2248,10 +1236,7 @@ hipError_t launch_part_chain(const DevCode &c, const BpLaunch &a, const BpLaunch
   BpLaunch bf = a;  // barrier-exchange FAST launch: the whole batch, or the tagged launch's deferrals
   bool reset = a.reset_abort;
   if (tagged) {
-    if constexpr (kG == kP2G && T_ == kP2T)
-      e = launch_part2_t<SYN>(c, d, s, fast, groups, reset);
-    else
-      e = launch_part_t<kG, T_, R_, R_, X_, SYN, true, false>(c, d, s, fast, groups, reset);
+    e = launch_part_t<kG, T_, R_, R_, X_, SYN, true, false>(c, d, s, fast, groups, reset);
     if (e != hipSuccess) return e;
     bf.cw_idx = d.defer_idx;
     bf.B_dev = d.defer_cnt;
@@ -2265,78 +1250,44 @@ hipError_t launch_part_chain(const DevCode &c, const BpLaunch &a, const BpLaunch
   return launch_part_t<kG, T_, R_, R_, X_, SYN, false, true>(c, be, s, 0, groups, false);
 }
 
-// Kernel choice and tiling.  Default: the partitioned kernel (groups of 4,
-// KML_PART = threads per workgroup: 512, 768 or 1024) when the context built a
-// partition plan.  KML_COOP = "G,T" selects the global-slot kernel instead
-// (workgroups per codeword, threads per workgroup), for A/B measurements.
-struct CoopCfg {
-  bool part;
-  int G, T;
-};
-CoopCfg coop_cfg(const DevCode &c) {
-  CoopCfg k{(c.pt_G == 4 || c.pt_G == kP2G) && c.pt_vn != nullptr, 4, 512};
-  if (k.part) {
-    k.G = c.pt_G;
-    k.T = 1024;
-    // groups of 8: two codewords per CU, either in one workgroup (bp_part2_kernel,
-    // default) or as two workgroups of 512 threads (KML_PART_MODE=2wg, A/B)
-    if (k.G == kP2G)
-      if (const char *e = getenv("KML_PART_MODE"))
-        if (e[0] == '2' && e[1] == 'w') k.T = 512;
+// Tiling of the partitioned kernel: KML_PART = threads per workgroup (512,
+// 768 or 1024; default 1024).
+int part_threads() {
+  if (const char *e = getenv("KML_PART")) {
+    const int t = atoi(e);
+    if (t == 512 || t == 768 || t == 1024) return t;
   }
-  if (const char *e = getenv("KML_COOP")) {
-    int g = 0, t = 0;
-    if (sscanf(e, "%d,%d", &g, &t) == 2 && (g == 4 || g == 8) && (t == 512 || t == 1024)) k = {false, g, t};
-  }
-  if (k.part && k.G == 4)
-    if (const char *e = getenv("KML_PART")) {
-      const int t = atoi(e);
-      if (t == 512 || t == 768 || t == 1024) k.T = t;
-    }
-  return k;
+  return 1024;
 }
 
 }  // namespace
 
-size_t bp_coop_sync_bytes(int groups) { return part2_sync_offset(groups) + sizeof(Part2Sync) * (size_t)groups; }
+size_t bp_coop_sync_bytes(int groups) { return part_defer_offset(groups) + 16; }
 
 int bp_part_group_size(int N, int M, int E, int dv_max, int dc_max, int regular) {
   if (!regular || dv_max != 3 || dc_max != 6 || (long long)E * 16 + 16 + N <= 160 * 1024) return 0;
-  int G = KML_PART_G_DEFAULT;  // KML_PART_G=4 / 8 (A/B)
-  if (const char *e = getenv("KML_PART_G")) {
-    if (atoi(e) == 4) G = 4;
-    if (atoi(e) == 8) G = kP2G;
-  }
-  for (;; G = 4) {
-    if (!(N % G || M % G || (N / G) % 16)) {
-      const int NG = N / G, MG = M / G;
-      // tilings: G = 4 up to 2048 columns and half-rows per member, G = 8 up
-      // to 1024 (T = 1024, one each); the LDS check including the mirror
-      // slots is part_plan_fits (after planning)
-      const int cap = G == 4 ? 2048 : 1024;
-      if ((long long)MG * 6 * 16 + N <= 160 * 1024 && NG <= cap && 2 * MG <= cap) return G;
-    }
-    if (G == 4) return 0;
-  }
+  const int G = kPartG;
+  if (N % G || M % G || (N / G) % 16) return 0;
+  // tilings up to 2048 columns and half-rows per member; the LDS check
+  // including the mirror slots is part_plan_fits (after planning)
+  const int NG = N / G, MG = M / G;
+  return ((long long)MG * 6 * 16 + N <= 160 * 1024 && NG <= 2048 && 2 * MG <= 2048) ? G : 0;
 }
 
 bool part_plan_fits(int G, int N, int M, int E, int ncut, int mirror_max, int xmax) {
   const long long lds = ((long long)M / G * 6 + mirror_max + kPartDummy) * 16 + N;
-  return lds <= 160 * 1024 && 3LL * ncut <= 2LL * E && xmax <= 2 * 1024 && (G != kP2G || part2_fits(N, M, ncut));
+  return G == kPartG && lds <= 160 * 1024 && 3LL * ncut <= 2LL * E && xmax <= 2 * 1024;
 }
 
+// Codes without a partition plan (or whose plan did not fit) decode on the
+// generic bp_kernel (launch_bp_coop returns hipErrorNotSupported).
 int bp_coop_groups(const DevCode &c) {
   if (!c.regular || !c.reg_pos || c.dv_max != 3 || c.dc_max != 6 || bp_uses_lds(c)) return 0;
-  const CoopCfg k = coop_cfg(c);
-  if (!k.part) {
-    const int R = 8192 / (k.G * k.T);  // columns (and half-rows) per thread of the instantiated tilings
-    if ((c.N + k.G - 1) / k.G > R * k.T || (2 * c.M + k.G - 1) / k.G > R * k.T) return 0;
-  }
+  if (c.pt_G != kPartG || c.pt_vn == nullptr) return 0;
   int dev = 0, ncu = 0;
   hipGetDevice(&dev);
   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  const int per_cu = k.part && k.G == kP2G && k.T == 512 ? 2 : 1;  // KML_PART_MODE=2wg: two workgroups per CU
-  return (per_cu * ncu / (8 * k.G)) * 8;  // 8 XCDs, groups of G per XCD
+  return (ncu / (8 * kPartG)) * 8;  // 8 XCDs, groups of 4 per XCD
 }
 
 #ifdef KML_STAMPS
@@ -2352,7 +1303,7 @@ extern "C" int kml_debug_part_stamps(unsigned long long *out, int reset) {
 namespace kml {
 #endif
 
-const char *bp_coop_family(const DevCode &c) { return coop_cfg(c).part ? "bp_part_kernel" : "bp_coop_kernel"; }
+const char *bp_coop_family(const DevCode &) { return "bp_part_kernel"; }
 
 hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s) {
   const int groups = bp_coop_groups(c);
@@ -2360,21 +1311,20 @@ hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s) {
   if (const char *k = getenv("KML_BP_KERNEL"))
     if (k[0] == 'g') return hipErrorNotSupported;
   const int fast = bp_fast_mode(c);
-  const CoopCfg k = coop_cfg(c);
-  if (k.part) {
+  const int T = part_threads();
+  {
     // exchange entries per thread: every member's lists must fit RX * T
     int xmax = 0;
     for (int m = 0; m < c.pt_G; m++) xmax = std::max(xmax, std::max(c.pt_xr_n[m], c.pt_xc_n[m]));
     // Tagged exchange (default): one launch for the FAST codewords of same-XCD
     // groups, then a barrier-exchange launch over the codewords it deferred
     // (list and count in scratch past the groups' mailboxes / sync blocks).
-    bool tagged = (k.G == kP2G && k.T == kP2T ? part2_usable(c) : part_tagged_fits(c.E, c.pt_ncut)) && fast;
+    bool tagged = part_tagged_fits(c.E, c.pt_ncut) && fast;
     if (const char *t = getenv("KML_PART_TAGGED"))
       if (t[0] == '0') tagged = false;
     BpLaunch d = a;
     if (tagged) {
-      // the tagged launch's defer list (and the two-slot kernel's eligibility
-      // bytes) past the groups' mailboxes
+      // the tagged launch's defer list past the groups' mailboxes
       const long long mb = (long long)groups * part_group_stride(c);
       if ((a.gslots_cap - mb) * 16 < 5LL * a.B + 64) return hipErrorNotSupported;
       d.defer_idx = reinterpret_cast<int32_t *>(a.gslots + (size_t)mb);
@@ -2383,27 +1333,15 @@ hipError_t launch_bp_coop(const DevCode &c, const BpLaunch &a, hipStream_t s) {
       if (e != hipSuccess) return e;
     }
 #define KML_PART_CASE(G_, T_, R_, X_)                \
-  if (k.G == G_ && k.T == T_ && xmax <= X_ * T_) \
+  if (T == T_ && xmax <= X_ * T_) \
     return a.syn ? launch_part_chain<G_, T_, R_, X_, true>(c, a, d, s, fast, groups, tagged) \
                  : launch_part_chain<G_, T_, R_, X_, false>(c, a, d, s, fast, groups, tagged);
     KML_PART_CASE(4, 512, 4, 4)
     KML_PART_CASE(4, 768, 3, 3)
     KML_PART_CASE(4, 1024, 2, 2)
-    KML_PART_CASE(8, 1024, 1, 2)
-    KML_PART_CASE(8, 512, 2, 3)
 #undef KML_PART_CASE
     return hipErrorNotSupported;
   }
-#define KML_COOP_CASE(G_, T_, R_)                                                                               \
-  if (k.G == G_ && k.T == T_)                                                                                  \
-    return a.syn ? launch_coop_t<G_, T_, R_, R_, true>(c, a, s, fast, groups)                                  \
-                 : launch_coop_t<G_, T_, R_, R_, false>(c, a, s, fast, groups);
-  KML_COOP_CASE(4, 512, 4)
-  KML_COOP_CASE(4, 1024, 2)
-  KML_COOP_CASE(8, 512, 2)
-  KML_COOP_CASE(8, 1024, 1)
-#undef KML_COOP_CASE
-  return hipErrorNotSupported;
 }
 
 hipError_t bp_coop_raise_abort(const BpLaunch &a, int groups, hipStream_t s) {

@@ -87,6 +87,7 @@ struct kml_ctx {
   long long part_cut = 0;   // cut edges of the partition plan (partitioned cooperative kernel)
   bool coop_pending = false;  // a cooperative launch whose abort word is unchecked
   bool coop_this_call = false;  // the current API call made a cooperative launch (fail() settles it)
+  bool coop_inherited = false;  // ... on top of an earlier call's unchecked launch (the abort word is shared)
   int inject_abort = -1;      // test hook (kml_debug_inject_abort): raise the abort after the n-th coop launch
   bool inject_fail = false;   // test hook (kml_debug_inject_abort(-2)): ... and fail that call before its sync
   kml::RcclComm *comm = nullptr;  // counter all-reduce over the ranks (kml_comm_init)
@@ -121,17 +122,32 @@ namespace {
 // the call's error), so the next call's first launch clears it instead of
 // inheriting it (a stale timeout reported against a healthy call).  A pending
 // launch of an EARLIER call (kml_sim_decode with do_sync = 0) stays pending
-// for its own kml_sync.
+// for its own kml_sync: when this call's launches shared its abort word
+// (coop_inherited) and the word is set, it stays pending.
 int fail(kml_ctx *c, int code, const std::string &msg) {
   if (c) {
     c->err = msg;
     if (c->coop_pending && c->coop_this_call) {
-      if (c->stream) (void)hipStreamSynchronize(c->stream);
-      c->coop_pending = false;
+      bool keep = false;
+      if (c->stream) {
+        (void)hipStreamSynchronize(c->stream);
+        if (c->coop_inherited) {
+          kml::BpLaunch a;
+          a.gsync = c->d_gsync.p;
+          keep = kml::bp_coop_aborted(a, c->coop_groups, c->stream);
+        }
+      }
+      c->coop_pending = keep;
       c->coop_this_call = false;
     }
   }
   return code;
+}
+
+// Every entry point that takes a context starts here: a new API call, so the
+// cooperative launches fail() settles are only this call's.
+inline void call_begin(kml_ctx *c) {
+  if (c) c->coop_this_call = false;
 }
 
 int hip_fail(kml_ctx *c, hipError_t e, const char *what) {
@@ -421,7 +437,10 @@ int run_bp(kml_ctx *c, kml::BpLaunch a, int &slot_out, int reuse = -1) {
   // last sync(): a timeout in any launch before the check (e.g. chunk 0 of a
   // chunked host-buffer call) stays set until sync() reports it
   a.reset_abort = !c->coop_pending;
-  if (c->coop_groups > 0) c->coop_pending = c->coop_this_call = true;
+  if (c->coop_groups > 0) {
+    if (!c->coop_this_call) c->coop_inherited = c->coop_pending;  // the call's first cooperative launch
+    c->coop_pending = c->coop_this_call = true;
+  }
   Timer t(c, "bp", slot, (double)a.B * 8.0 * c->code.cc_len);
   const char *msg = nullptr;
   hipError_t e = kml::launch_bp(c->dc, a, c->stream, &msg, &c->bp_family);
@@ -499,7 +518,6 @@ int sync(kml_ctx *c) {
 
 int need_gpu(kml_ctx *c) {
   if (c->device < 0 || !c->stream) return fail(c, KML_E_ARG, "host-only context (device < 0): no GPU operations");
-  c->coop_this_call = false;  // a new API call (every GPU entry point starts here)
   return KML_OK;
 }
 
@@ -1004,6 +1022,7 @@ int kml_encode(const kml_ctx *c, const uint8_t *uu, uint8_t *cc, int B) {
 
 int kml_bp_decode(kml_ctx *c, const double *p0, int B, int iter_count, uint8_t *uu_hat, int32_t *ret, uint8_t *cc_hat,
                   double *syn, int flags) {
+  call_begin(c);
   if (!c || !p0 || B < 0 || iter_count < 0) return fail(c, KML_E_ARG, "kml_bp_decode: bad argument");
   if (B == 0) return KML_OK;
   TRY(need_gpu(c));
@@ -1041,6 +1060,7 @@ int kml_bp_decode(kml_ctx *c, const double *p0, int B, int iter_count, uint8_t *
 }
 
 int kml_demap(kml_ctx *c, const double *y, const double *h, double var, int B, double *p0, int flags) {
+  call_begin(c);
   if (!c || !y || !h || !p0 || B < 0) return fail(c, KML_E_ARG, "kml_demap: bad argument");
   if (B == 0) return KML_OK;
   TRY(need_gpu(c));
@@ -1063,6 +1083,7 @@ int kml_demap(kml_ctx *c, const double *y, const double *h, double var, int B, d
 }
 
 int kml_kmeans(kml_ctx *c, const double *y, int B, int iters, double *h_hat, double *h4, int flags) {
+  call_begin(c);
   if (!c || !y || B < 0 || iters < 0) return fail(c, KML_E_ARG, "kml_kmeans: bad argument");
   if (B == 0) return KML_OK;
   TRY(need_gpu(c));
@@ -1089,6 +1110,7 @@ int kml_kmeans(kml_ctx *c, const double *y, int B, int iters, double *h_hat, dou
 }
 
 int kml_kmeans_state(kml_ctx *c, const double *y, int B, int iters, double *clusters, int32_t *idx, int flags) {
+  call_begin(c);
   if (!c || !y || B < 0 || iters < 0) return fail(c, KML_E_ARG, "kml_kmeans_state: bad argument");
   if (B == 0) return KML_OK;
   TRY(need_gpu(c));
@@ -1288,6 +1310,7 @@ int kml_comm_unique_id(uint8_t *id) {
 }
 
 int kml_comm_init(kml_ctx *c, const uint8_t *id, int world, int rank) {
+  call_begin(c);
   if (!c || !id || world < 1 || rank < 0 || rank >= world) return fail(c, KML_E_ARG, "kml_comm_init: bad argument");
   TRY(need_gpu(c));
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
@@ -1320,6 +1343,7 @@ int kml_comm_allreduce_u64(kml_ctx *c, uint64_t *vals, int n) { return comm_allr
 int kml_comm_allreduce_f64(kml_ctx *c, double *vals, int n) { return comm_allreduce(c, vals, n, true); }
 
 int kml_debug_inject_abort(kml_ctx *c, int nth) {
+  call_begin(c);
   if (!c) return KML_E_ARG;
   c->inject_fail = nth == -2;
   c->inject_abort = nth == -2 ? 0 : nth;
@@ -1328,6 +1352,7 @@ int kml_debug_inject_abort(kml_ctx *c, int nth) {
 
 int kml_decode_frames(kml_ctx *c, const double *y, const double *true_h, double snr, int B, uint8_t *uu_hat,
                       int32_t *chosen, double *metrics, int32_t *ret, double *h_hat, int flags) {
+  call_begin(c);
   if (!c || !y || !uu_hat || B < 0) return fail(c, KML_E_ARG, "kml_decode_frames: bad argument");
   if (B == 0) return KML_OK;
   TRY(need_gpu(c));
@@ -1389,6 +1414,7 @@ int kml_decode_frames(kml_ctx *c, const double *y, const double *true_h, double 
 
 int kml_decode_candidates(kml_ctx *c, const double *y, const double *h_hats, int nc, double snr, int B,
                           uint8_t *uu_hat, int32_t *chosen, double *metrics, int32_t *ret, int flags) {
+  call_begin(c);
   if (!c || !y || !h_hats || !uu_hat || B < 0 || nc < 1 || nc > 4)
     return fail(c, KML_E_ARG, "kml_decode_candidates: bad argument (need 1 <= nc <= 4)");
   // one estimate: Decoder computes no metric (kmcodec.cc:66-67); GetHistogramData
@@ -1432,6 +1458,7 @@ int kml_decode_candidates(kml_ctx *c, const double *y, const double *h_hats, int
 }
 
 int kml_count_errors(kml_ctx *c, const uint8_t *uu, const uint8_t *uu_hat, int B, uint64_t *counters, int flags) {
+  call_begin(c);
   if (!c || !uu || !uu_hat || !counters || B < 0) return fail(c, KML_E_ARG, "kml_count_errors: bad argument");
   if (B == 0) return KML_OK;
   TRY(need_gpu(c));
@@ -1451,6 +1478,7 @@ int kml_count_errors(kml_ctx *c, const uint8_t *uu, const uint8_t *uu_hat, int B
 }
 
 int kml_sim_generate(kml_ctx *c, double snr, uint64_t seed, uint64_t first_cw, int B) {
+  call_begin(c);
   if (!c || B < 0) return fail(c, KML_E_ARG, "kml_sim_generate: bad argument");
   TRY(need_gpu(c));
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
@@ -1501,6 +1529,7 @@ int sim_receive(kml_ctx *c, double snr, int blind, bool histogram, int &slot) {
 }  // namespace
 
 int kml_sim_decode(kml_ctx *c, double snr, int blind, uint64_t *counters, int do_sync) {
+  call_begin(c);
   if (!c) return KML_E_ARG;
   if (!do_sync && counters) return fail(c, KML_E_ARG, "counters need sync != 0");
   TRY(need_gpu(c));
@@ -1520,6 +1549,7 @@ int kml_sim_decode(kml_ctx *c, double snr, int blind, uint64_t *counters, int do
 
 int kml_sim_decode_ex(kml_ctx *c, double snr, int blind, int histogram, int32_t *cw_err, double *metrics,
                       uint64_t *counters) {
+  call_begin(c);
   if (!c) return KML_E_ARG;
   TRY(need_gpu(c));
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
@@ -1570,6 +1600,7 @@ int kml_run_config(const kml_ctx *c, double *f, int64_t *n) {
 }
 
 int kml_sync(kml_ctx *c) {
+  call_begin(c);
   if (!c) return KML_E_ARG;
   TRY(need_gpu(c));
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
@@ -1578,6 +1609,7 @@ int kml_sync(kml_ctx *c) {
 
 int kml_sim_load(kml_ctx *c, double snr, const uint8_t *uu, const double *y, const double *h, int B,
                  uint64_t first_cw) {
+  call_begin(c);
   if (!c || B < 0 || (B > 0 && (!uu || !y || !h))) return fail(c, KML_E_ARG, "kml_sim_load: bad argument");
   TRY(need_gpu(c));
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
@@ -1604,6 +1636,7 @@ int kml_sim_load(kml_ctx *c, double snr, const uint8_t *uu, const double *y, con
 }
 
 int kml_sim_frames(kml_ctx *c, uint8_t *uu, double *y, double *h) {
+  call_begin(c);
   if (!c) return KML_E_ARG;
   TRY(need_gpu(c));
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
@@ -1622,12 +1655,14 @@ int kml_sim_frames(kml_ctx *c, uint8_t *uu, double *y, double *h) {
 }
 
 int kml_prof_enable(kml_ctx *c, int on) {
+  call_begin(c);
   if (!c) return KML_E_ARG;
   c->prof = on != 0;
   return KML_OK;
 }
 
 int kml_prof_reset(kml_ctx *c) {
+  call_begin(c);
   if (!c) return KML_E_ARG;
   drain_profile(c);
   c->stats.clear();
@@ -1635,6 +1670,7 @@ int kml_prof_reset(kml_ctx *c) {
 }
 
 int kml_prof_read_flops(kml_ctx *c, const char *stage, double *alg_flops) {
+  call_begin(c);
   if (!c || !stage || !alg_flops) return KML_E_ARG;
   if (c->device >= 0) hipSetDevice(c->device);
   drain_profile(c);
@@ -1644,6 +1680,7 @@ int kml_prof_read_flops(kml_ctx *c, const char *stage, double *alg_flops) {
 }
 
 int kml_prof_read(kml_ctx *c, const char *stage, int64_t *launches, double *total_ms, double *alg_bytes) {
+  call_begin(c);
   if (!c || !stage) return KML_E_ARG;
   if (c->device >= 0) hipSetDevice(c->device);
   drain_profile(c);
@@ -1662,6 +1699,7 @@ int kml_ref_frames(const kml_ctx *c, int64_t *state, double snr, int n, uint8_t 
 }
 
 int kml_log_probe(kml_ctx *c, const double *in, int n, double *out) {
+  call_begin(c);
   if (!c || !in || !out || n < 0) return KML_E_ARG;
   TRY(need_gpu(c));
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
@@ -1674,6 +1712,7 @@ int kml_log_probe(kml_ctx *c, const double *in, int n, double *out) {
 }
 
 int kml_math_probe(kml_ctx *c, const double *in, int n, double *out) {
+  call_begin(c);
   if (!c || !in || !out || n < 0) return KML_E_ARG;
   TRY(need_gpu(c));
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
@@ -1686,6 +1725,7 @@ int kml_math_probe(kml_ctx *c, const double *in, int n, double *out) {
 }
 
 int kml_div_probe(kml_ctx *c, const double *in, int n, double *out) {
+  call_begin(c);
   if (!c || !in || !out || n < 0) return KML_E_ARG;
   TRY(need_gpu(c));
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
