@@ -18,6 +18,7 @@
 // throughput path uses the counter-based generator in framegen.hip instead.
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 #include <vector>
 
 #include "../../include/kmldpc_amd.h"
@@ -110,6 +111,7 @@ int ref_frames(const LdpcCode &code, const Modem &modem, int64_t *state, double 
     uint8_t *uu = uu_out + (size_t)b * K;
     kml_get_bit_str(state, uu, K);
     code.encode(uu, cc.data());
+    if (!code.active) memset(uu, 0, K);  // the inactive Encoder zeroes uu too (binaryldpccodec.cc:157-158)
     double h[2];
     kml_lcg_normal(state, h, 2);
     const double hr = h[0] * s5, hi = h[1] * s5;

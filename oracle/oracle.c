@@ -307,9 +307,11 @@ void orc_code_graph(const orc_code *c, int32_t *row_ptr, int32_t *row_col, int32
 
 /* ------------------------------------------------------------- Encoder */
 
-void orc_encode(const orc_code *c, const int32_t *uu, int32_t *cc) {
+void orc_encode(const orc_code *c, int32_t *uu, int32_t *cc) {
   const int N = c->N, chk = c->chk, K = c->K, W = c->W;
-  if (!c->enc) { /* binaryldpccodec.cc:156-161: all-zero codeword */
+  if (!c->enc) { /* binaryldpccodec.cc:156-161, binary5gldpccodec.cc:103-108: the inactive
+                    encoder zeroes uu (an in/out argument) and the codeword */
+    for (int i = 0; i < K; i++) uu[i] = 0;
     for (int i = 0; i < c->cc_len; i++) cc[i] = 0;
     return;
   }

@@ -41,7 +41,7 @@ void orc_code_graph(const orc_code *c, int32_t *row_ptr, int32_t *row_col, int32
 
 /* Encoder: binaryldpccodec.cc:144-162 / binary5gldpccodec.cc:86-109.
  * uu[K] -> cc[cc_len]; values 0/1. */
-void orc_encode(const orc_code *c, const int32_t *uu, int32_t *cc);
+void orc_encode(const orc_code *c, int32_t *uu, int32_t *cc);
 
 /* Sum-product BP: binaryldpccodec.cc:165-278 / binary5gldpccodec.cc:112-232.
  * p0[cc_len] = P(bit=0).  Writes uu_hat[K], cc_hat[Ncol] (may be NULL) and

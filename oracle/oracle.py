@@ -93,7 +93,7 @@ class Code:
         return rp, rc, cp, cs
 
     def encode(self, uu):
-        uu = np.ascontiguousarray(uu, np.int32)
+        uu = np.array(uu, np.int32)  # a copy: the inactive encoder zeroes its uu (binaryldpccodec.cc:157-158)
         cc = np.zeros(self.cc_len, np.int32)
         lib().orc_encode(self.h, _p(uu), _p(cc))
         return cc

@@ -59,6 +59,15 @@ CASES = {
     "peg8064_64qam_blind": ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, False, 20, 6.77, 60, True),
     "peg8064_64qam_known": ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, True, 20, 6.77, 40, True),
     "peg2304_16qamphi1_blind": ("PEG2304regular0.5.txt", "4bit_16QAM_phi1.txt", False, False, 20, 8.0, 100, True),
+    # the last shipped constellation (config/4bit_16QAM_phi2.txt), blind and known
+    "peg2304_16qamphi2_blind": ("PEG2304regular0.5.txt", "4bit_16QAM_phi2.txt", False, False, 20, 14.0, 100, True),
+    "peg2304_16qamphi2_known": ("PEG2304regular0.5.txt", "4bit_16QAM_phi2.txt", False, True, 20, 6.0, 100, True),
+    # [ldpc] active = false: no SystemMatrixH, the file-order graph, all-zero
+    # codewords (binaryldpccodec.cc:125-127, 148-161; binary5gldpccodec.cc:75-76, 92-108)
+    "peg2304_qpsk_known_inactive": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, True, 20, 1.0, 200, False),
+    "peg2304_qpsk_blind_inactive": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.0, 200, False),
+    "bg2_16qam_known_inactive": ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, True, 50, 4.0, 100, False),
+    "bg2_16qam_blind_inactive": ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, False, 50, 5.01, 60, False),
 }
 
 # soft syndrome metric ([xcodec] metric_type = true): name -> (matrix, modem, 5g,
