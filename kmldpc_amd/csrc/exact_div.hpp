@@ -198,4 +198,24 @@ __device__ __forceinline__ double div_rn(double n, double s) {
   else return div_rn_cold(n, s);
 }
 
+// div_rn with the divisor's reciprocal taken by the caller (y = dd_rcp(s),
+// e.g. once for several quotients by one divisor, or ahead of the numerator):
+// the same operations on the same values.
+template <bool INLINE_RARE = false>
+__device__ __forceinline__ double div_rn_y(double n, double s, const DdRcp &y) {
+  const double an = fabs(n), as = fabs(s);
+  if (__builtin_expect((an >= 0x1p-969) & (an < 0x1p1000) & (as >= 0x1p-1000) & (as < 0x1p1000), 1)) {
+    double q = dd_quot(n, y);
+    const double aq = fabs(q);
+    if (__builtin_expect((aq >= 0x1p-1020) & (aq < 0x1p1020), 1)) {
+      const double r = fma(-q, s, n);
+      const long long step = ((r > 0.0) == (s > 0.0)) == (q > 0.0) ? 1 : -1;
+      const double qn = __longlong_as_double(__double_as_longlong(q) + step);
+      return fabs(fma(-qn, s, n)) < fabs(r) ? qn : q;
+    }
+  }
+  if constexpr (INLINE_RARE) return div_rn_rare(n, s);
+  else return div_rn_cold(n, s);
+}
+
 }  // namespace kml

@@ -269,7 +269,7 @@ def test_cn_reciprocal_exhaustive(data_dir):
 def test_bp_golden_vectors(case, data_dir):
     """Decode the reference's own P0 vectors: every output bit-exact."""
     hdr, z = load_case(case)
-    ctx = ctx_for(data_dir, hdr["matrix"], hdr["modem"], bool(hdr["is5g"]), hdr["max_iter"])
+    ctx = ctx_for(data_dir, hdr["matrix"], hdr["modem"], bool(hdr["is5g"]), hdr["max_iter"], bool(hdr["active"]))
     p0 = z["v_p0"]
     B = p0.shape[0]
     syn0 = np.full((B, ctx.M), -1.0)
@@ -453,14 +453,61 @@ def test_kmeans_adversarial_ties(data_dir, modem):
         assert np.array_equal(hh[b], ref, equal_nan=True), b
 
 
+@pytest.mark.parametrize("mode", ["default", "one_chain_per_wave", "owned_words"])
+@pytest.mark.parametrize("modem", ["2bits_QPSK.txt", "4bit_16QAM_Gray.txt", "6bits_64QAM_Gray.txt"])
+def test_kmeans_word_scan_adversarial(data_dir, modem, mode, monkeypatch):
+    """The fused k-means' word scan (kmeans.hip km_word_sum: per-word grid sums
+    cached across iterations, tie parities, binade exits) against the
+    oracle's sequential cumulative sums (kmeans.cc:33-46), on inputs built to
+    hit its corner cases: noise on a coarse dyadic grid (ties in nearly every
+    word), a cluster-0 centre on an axis (sums that change sign), tiny and huge
+    channels (extreme binades), NaN / inf symbols and realistic frames; both
+    lane layouts (KML_KM_HALF=1: both chains in one wave, 0: one per wave) and
+    both splits of the assignment (KML_KM_BAL=1: flagged words by rank, 0: each
+    wave its own words)."""
+    monkeypatch.setenv("KML_KM_HALF", "0" if mode == "one_chain_per_wave" else "1")
+    monkeypatch.setenv("KML_KM_BAL", "0" if mode == "owned_words" else "1")
+    matrix = "PEG8064regular0.5.txt" if "64QAM" in modem else "PEG2304regular0.5.txt"
+    ctx = ctx_for(data_dir, matrix, modem, False)
+    om = O.Modem(os.path.join(data_dir, modem))
+    pts = om.points.reshape(-1, 2) @ [1, 1j]
+    rng = np.random.default_rng(41)
+    S, B = ctx.S, 20
+    y = np.zeros((B, S, 2))
+    for b in range(B):
+        kind = b % 5
+        hc = [1.0, 1j, 1e-200 * complex(*rng.normal(size=2)), 1e150 * complex(*rng.normal(size=2)),
+              complex(*rng.normal(size=2))][kind]
+        sym = pts[rng.integers(0, len(pts), S)]
+        if kind == 0:  # dyadic noise: the grid sums hit exact ties
+            noise = (rng.integers(-40, 40, S) + 1j * rng.integers(-40, 40, S)) * 2.0 ** -7
+        else:
+            noise = 0.3 * abs(hc) * (rng.normal(size=S) + 1j * rng.normal(size=S))
+        zz = sym * hc + noise
+        if b == 9:
+            zz[rng.integers(0, S, 3)] = np.nan
+        if b == 14:
+            zz[rng.integers(0, S, 2)] = np.inf
+        y[b, :, 0], y[b, :, 1] = zz.real, zz.imag
+    hh, h4 = ctx.kmeans(y)
+    for b in range(B):
+        ref = O.kmeans_hhat(y[b], om.points)
+        assert np.array_equal(hh[b], ref, equal_nan=True), b
+    oc = oracle_for(data_dir, matrix, False)
+    _, _, _, yr = O.gen_frames(oc, om, 6.77 if "64QAM" in modem else 2.0, 12, state=77)
+    hh, _ = ctx.kmeans(yr)
+    for b in range(yr.shape[0]):
+        assert np.array_equal(hh[b], O.kmeans_hhat(yr[b], om.points)), b
+
+
 @pytest.mark.parametrize("case", CASES)
 def test_decode_frames_vs_reference_stream(case, data_dir):
     """KmCodec::Decoder on the reference's own frames (regenerated bit-exactly
     by the oracle, pinned by the y CRCs): chosen candidate, BP return value,
     decoded bits and error counts equal the reference's."""
     hdr, z = load_case(case)
-    ctx = ctx_for(data_dir, hdr["matrix"], hdr["modem"], bool(hdr["is5g"]), hdr["max_iter"])
-    oc = oracle_for(data_dir, hdr["matrix"], bool(hdr["is5g"]), hdr["max_iter"])
+    ctx = ctx_for(data_dir, hdr["matrix"], hdr["modem"], bool(hdr["is5g"]), hdr["max_iter"], bool(hdr["active"]))
+    oc = oracle_for(data_dir, hdr["matrix"], bool(hdr["is5g"]), hdr["max_iter"], bool(hdr["active"]))
     om = O.Modem(os.path.join(data_dir, hdr["modem"]))
     n = hdr["ncw"]
     uu, cc, th, y = O.gen_frames(oc, om, hdr["snr"], n)
@@ -524,45 +571,27 @@ def test_dispatch_takes_the_specialised_kernel(data_dir, matrix, modem, is5g, ma
     assert ctx.bp_kernel() == FAMILY[matrix]
 
 
-def test_global_slot_cooperative_kernel_still_exact(data_dir, monkeypatch):
-    """KML_COOP=G,T selects the global-slot cooperative kernel (the partitioned
-    kernel's predecessor, kept for A/B): still bit-exact on PEG8064."""
-    monkeypatch.setenv("KML_COOP", "4,512")
-    ctx = ctx_for(data_dir, "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 20)
-    oc = oracle_for(data_dir, "PEG8064regular0.5.txt", False, 20)
-    rng = np.random.default_rng(21)
-    p0 = rng.uniform(0.1, 0.9, (5, ctx.cc_len))
-    r = ctx.bp_decode(p0, cc_hat=True)
-    assert ctx.bp_kernel() == "bp_coop_kernel"
-    for i in range(len(p0)):
-        ret, uh, cch, _ = oc.bp_decode(p0[i])
-        assert r["ret"][i] == ret and np.array_equal(r["cc_hat"][i], cch), i
-
-
-@pytest.mark.parametrize("group", ["8", "4"])
 @pytest.mark.parametrize("tagged", ["1", "0"])
-def test_partitioned_kernel_tagged_exchange_and_deferral(data_dir, monkeypatch, tagged, group):
-    """The partitioned kernels' tagged exchange (FAST codewords: direct mailbox
-    stores, tag polling, per-iteration early-stop flags) — groups of 8 with two
-    codewords in flight per group (bp_part2_kernel, KML_PART_G=8) and groups
-    of 4 with one (KML_PART_G=4) — and the barrier-exchange launch they defer the
-    other codewords to: a PEG8064 batch with two codewords outside the
-    fast-division domain (-0.0 / subnormal priors) among FAST ones, iteration
-    budgets 20 and 1, bit-exact against the oracle on ret, cc_hat and the soft
-    syndromes; KML_PART_TAGGED=0 (barrier exchange only) gives the same."""
+def test_partitioned_kernel_tagged_exchange_and_deferral(data_dir, monkeypatch, tagged):
+    """The partitioned kernel's tagged exchange (FAST codewords: direct mailbox
+    stores, tag polling, per-iteration early-stop flags; groups of 4) and the
+    barrier-exchange launch it defers the other codewords to: a PEG8064 batch
+    with two codewords outside the fast-division domain (-0.0 / subnormal
+    priors) among FAST ones, iteration budgets 20, 1 and 0, bit-exact against
+    the oracle on ret, cc_hat and the soft syndromes; KML_PART_TAGGED=0
+    (barrier exchange only) gives the same."""
     monkeypatch.setenv("KML_PART_TAGGED", tagged)
-    monkeypatch.setenv("KML_PART_G", group)  # fixed when the context builds its partition plan
     ctx = K.Context(matrix_file=os.path.join(data_dir, "PEG8064regular0.5.txt"),
                     modem_file=os.path.join(data_dir, "6bits_64QAM_Gray.txt"), is5g=False, active=True,
                     max_iter=20, device=0)
-    assert ctx.dims["part_group"] == int(group)
+    assert ctx.dims["part_group"] == 4
     oc = oracle_for(data_dir, "PEG8064regular0.5.txt", False, 20)
     rng = np.random.default_rng(33)
     B = 300
     p0 = np.clip(rng.normal(0.5, 0.28, (B, ctx.cc_len)), 0.02, 0.98)
     p0[7, ::5] = -0.0
     p0[23, 1::7] = 5e-320
-    for it in (20, 1):
+    for it in (20, 1, 0):
         r = ctx.bp_decode(p0, iter_count=it, cc_hat=True, syn=np.zeros((B, ctx.M)))
         assert ctx.bp_kernel() == "bp_part_kernel"
         for i in list(range(0, B, 13)) + [7, 23, B - 1]:
@@ -719,9 +748,8 @@ def test_kmeans_state_vs_reference(name, data_dir):
 @pytest.mark.gpu
 @pytest.mark.parametrize("modem", ["2bits_QPSK.txt", "4bit_16QAM_Gray.txt", "6bits_64QAM_Gray.txt"])
 def test_kmeans_cluster0_majority(data_dir, modem):
-    """Frames that put more than S/2 symbols into cluster 0, past the member
-    list's capacity (kmeans.hip: cap = S/2; n > cap sums cluster 0 straight
-    from the membership words): an all-zero codeword (every distance ties, the
+    """Frames that put more than S/2 symbols into cluster 0 (dense membership
+    words for the word scan): an all-zero codeword (every distance ties, the
     first minimum wins), every symbol on point 0 times h, and 60-95 % of the
     symbols near point 0 times h with the rest random.  h_hat, clusters and
     idx bit-exact against the oracle (kmeans.cc:15-84)."""
@@ -876,6 +904,24 @@ def test_error_return_after_coop_launch_leaves_next_call_clean(data_dir):
         assert np.array_equal(r1[k], r0[k]), k
 
 
+def test_pending_abort_survives_a_later_argument_error(data_dir):
+    """kml_sim_decode(sync=0) leaves its cooperative launch pending for
+    kml_sync.  A later call that fails on its arguments, before any GPU work,
+    must not settle (and drop) that launch's abort: kml_sync still reports it
+    (capi.cpp call_begin / fail()).  Then the context is clean again."""
+    ctx = ctx_for(data_dir, "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False)
+    ctx.sim_generate(6.0, 64, seed=5)
+    c0 = ctx.sim_decode(6.0, blind=False)
+    ctx.debug_inject_abort(0)
+    ctx.sim_decode(6.0, blind=False, sync=False)
+    cnt = np.zeros(8, np.uint64)
+    rc = K.lib().kml_sim_decode(ctx._h, 6.0, 0, K._p(cnt), 0)  # KML_E_ARG: counters need sync != 0
+    assert rc == -1
+    with pytest.raises(K.KmlError, match="aborted"):
+        ctx.sync()
+    assert ctx.sim_decode(6.0, blind=False) == c0
+
+
 # The exact path and the redo machinery (exact_div.hpp, DESIGN.md "Exact
 # division"): KML_NO_FAST=1 decodes every codeword on the exact path (div_rn
 # everywhere); KML_FORCE_REDO=1 treats every FAST decode as suspect, so each
@@ -892,7 +938,7 @@ EXACT_MODES = ["KML_NO_FAST", "KML_FORCE_REDO"]
 def test_exact_path_golden_vectors(case, data_dir, mode, monkeypatch):
     hdr, z = load_case(case)
     monkeypatch.setenv(mode, "1")
-    ctx = ctx_for(data_dir, hdr["matrix"], hdr["modem"], bool(hdr["is5g"]), hdr["max_iter"])
+    ctx = ctx_for(data_dir, hdr["matrix"], hdr["modem"], bool(hdr["is5g"]), hdr["max_iter"], bool(hdr["active"]))
     p0 = z["v_p0"]
     B = p0.shape[0]
     syn0 = np.full((B, ctx.M), -1.0)
@@ -931,3 +977,38 @@ def test_forced_redo_counts_and_counters(data_dir, monkeypatch):
     assert c1["redone"] == 1024
     for k in ("err_bit", "err_blk", "tot_bit", "tot_blk", "vn_phases", "cn_phases", "converged"):
         assert c1[k] == c0[k], k
+
+
+@pytest.mark.parametrize("modem", ["2bits_QPSK.txt", "4bit_16QAM_Gray.txt", "6bits_64QAM_Gray.txt"])
+def test_candidate_metric_screen_equals_exact_demap(data_dir, modem, monkeypatch):
+    """The candidate metric's single-precision screen (demap_common.hpp
+    hard_bits_screen: v_exp_f32, fma ordering, fminf, the fmin <= 64 and
+    2^20 gates) decides a hard bit only where the exact demapper agrees.  On
+    frames built to sit at its edges — symbols on decision boundaries (midpoints
+    of constellation points, tiny offsets), channels of |h| from 1e-3 to 1e4 —
+    the metrics and chosen candidates with the screen on equal those with every
+    symbol on the exact demapper (KML_CM_NOSCREEN=1)."""
+    matrix = "PEG8064regular0.5.txt" if "64QAM" in modem else "PEG2304regular0.5.txt"
+    ctx = ctx_for(data_dir, matrix, modem, False)
+    om = O.Modem(os.path.join(data_dir, modem))
+    pts = om.points.reshape(-1, 2) @ [1, 1j]
+    rng = np.random.default_rng(57)
+    S, B = ctx.S, 12
+    y = np.zeros((B, S, 2))
+    hh = np.zeros((B, 4, 2))
+    for b in range(B):
+        hc = complex(*rng.normal(size=2)) * [1e-3, 0.3, 1.0, 30.0, 1e4][b % 5]
+        i1, i2 = rng.integers(0, len(pts), S), rng.integers(0, len(pts), S)
+        mid = (pts[i1] + pts[i2]) / 2
+        off = rng.choice([0.0, 1e-12, -1e-9, 1e-6, 3e-4], S) * (rng.normal(size=S) + 1j * rng.normal(size=S))
+        zz = (np.where(rng.random(S) < 0.7, mid, pts[i1]) + off) * hc
+        y[b, :, 0], y[b, :, 1] = zz.real, zz.imag
+        h4 = O.rotations(np.array([hc.real, hc.imag]) * (1 + 1e-7 * rng.normal()))
+        hh[b] = np.asarray(h4).reshape(4, 2)
+    snr = 6.77 if "64QAM" in modem else 4.0
+    r_on = ctx.decode_candidates(y, hh, snr)
+    monkeypatch.setenv("KML_CM_NOSCREEN", "1")
+    r_off = ctx.decode_candidates(y, hh, snr)
+    assert np.array_equal(r_on["metrics"], r_off["metrics"])
+    assert np.array_equal(r_on["chosen"], r_off["chosen"])
+    assert np.array_equal(r_on["uu_hat"], r_off["uu_hat"])
