@@ -48,7 +48,6 @@ K = None  # kmldpc_amd, imported only in a rank process (after the launch decisi
 KERNEL_NOTES = {
     "bp_regular_kernel": "sum-product BP, messages LDS-resident",
     "bp_irregular_kernel": "sum-product BP, irregular degrees, messages LDS-resident",
-    "bp_coop_kernel": "sum-product BP, 4 workgroups per codeword, messages in L2",
     "bp_part_kernel": "sum-product BP, partitioned LDS slots + cut-edge mailboxes: 4 workgroups on one XCD per "
                       "codeword, tagged mailbox exchange",
     "bp_kernel": "sum-product BP, generic",

@@ -95,7 +95,15 @@ __device__ __forceinline__ void vn_cols(double2 *slots, const unsigned short *co
       const double t0 = unit ? al0[r][k] : al0[r][k] * b0[r];
       const double t1 = unit ? al1[r][k] : al1[r][k] * b1[r];
       double q0, q1;
-      if (unit)  // beta = (1, 1): t is the normalised alpha, its sum within ulps of 1 (bp_common.hpp rcp_near1)
+      if (unit && D == 1) {
+        // a degree-1 column's v2c is its prior (p, 1 - p) / (p + RN(1 - p)), a
+        // constant of the codeword: for a FAST prior p in [0, 1] the sum is
+        // exactly 1 (1 - p is exact for p >= 1/2; below, RN(1 - p) is within
+        // 2^-54 of 1 - p, and p + RN(1 - p) = 1 + d with |d| <= 2^-54 rounds
+        // to 1, the tie -2^-54 to the even 1), so the quotients are t0, t1
+        q0 = t0;
+        q1 = t1;
+      } else if (unit)  // beta = (1, 1): t is the normalised alpha, its sum within ulps of 1 (bp_common.hpp rcp_near1)
         div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
       else
         div2<FAST>(t0, t1, t0 + t1, q0, q1, sus);

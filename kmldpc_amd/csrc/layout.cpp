@@ -607,7 +607,12 @@ void place_waves(const std::vector<WaveItems> &pairs, const std::vector<WaveItem
   lpt(singles, single_of);
 }
 
-double vn_cost(int d) { return 3.0 * d - 1.0; }  // div2 steps of a column (forward d-1, backward 2d-1)
+// div2 steps of a column (forward d-1, backward 2d-1); a degree-1 column's
+// FAST v2c needs none (bp_irregular.hip vn_cols), only its hard decision
+#ifndef KML_IRR_VN_COST1
+#define KML_IRR_VN_COST1 2.0
+#endif
+double vn_cost(int d) { return d == 1 ? KML_IRR_VN_COST1 : 3.0 * d - 1.0; }
 double cn_cost(int d) { return 1.5 * d; }        // per half-row: advances + half the c2v outputs
 
 }  // namespace

@@ -33,7 +33,7 @@ from collections import defaultdict
 
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6
-BP_FAMILIES = ("bp_regular_kernel", "bp_irregular_kernel", "bp_coop_kernel", "bp_part_kernel")
+BP_FAMILIES = ("bp_regular_kernel", "bp_irregular_kernel", "bp_part_kernel")
 # kernels launched as a FAST dispatch + an EXACT dispatch over its deferrals (last template argument EXACT)
 CHAIN_FAMILIES = BP_FAMILIES + ("demap_kernel", "cand_metric_kernel")
 # resident waves per SIMD of each kernel family (block size / register limits)
@@ -44,8 +44,6 @@ def parse(name):
     """(family, variant) of a rocprofv3 kernel name; variant 'exact' marks a chain's last dispatch."""
     n = name.replace("kml::(anonymous namespace)::", "").replace("void ", "")
     fam = n.split("(")[0].split("<")[0].strip()
-    if fam == "bp_part2_kernel":  # the two-slot tagged launch (groups of 8) of the bp_part_kernel chain
-        return "bp_part_kernel", "fast_tagged"
     if fam not in CHAIN_FAMILIES or "<" not in n:
         return fam, ""
     targs = [t.strip() for t in n.split("<", 1)[1].split(">")[0].split(",")]
