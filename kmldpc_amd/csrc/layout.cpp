@@ -481,6 +481,22 @@ static bool plan_partition_uncached(const LdpcCode &L, int G, PartitionPlan &out
   // phase's bank conflicts (write bins of the slot, read bins of the c2v half:
   // bp_coop.hip part_c2v_half — bit 2 of the row for row slots, of the slot
   // index for mirror slots)
+  // each member's INTERIOR columns (every edge's row its own) last: the
+  // partitioned kernel runs them before the cut-edge c2v receive, the
+  // boundary columns after it (bp_coop.hip, KML_PART_SPLIT); the annealing
+  // below keeps the two runs apart
+  std::vector<int> nbound(G, NG);
+  for (int g = 0; g < G; g++) {
+    auto interior = [&](int j) {
+      for (int e = L.col_ptr[j]; e < L.col_ptr[j + 1]; e++)
+        if (best_r[col_rows[e]] != g) return false;
+      return true;
+    };
+    auto first = out.vn.begin() + (size_t)g * NG, last = first + NG;
+    nbound[g] = (int)(std::stable_partition(first, last, [&](int j) { return !interior(j); }) - first);
+  }
+  out.interior = 0;
+  for (int g = 0; g < G; g++) out.interior += NG - nbound[g];
   if (KML_PART_ANNEAL) {
     std::vector<uint8_t> wb((size_t)N * dv), rb((size_t)N * dv);
     for (int j = 0; j < N; j++)
@@ -491,12 +507,15 @@ static bool plan_partition_uncached(const LdpcCode &L, int G, PartitionPlan &out
         rb[(size_t)j * dv + k] = (uint8_t)(((a + 8 * half) >> 3) & 31);
       }
     out.anneal_initial = out.anneal_final = 0;
-    for (int g = 0; g < G; g++) {
-      const auto c = anneal_vn_order(out.vn, g * NG, (g + 1) * NG, dv, wb, rb, 0x9E3779B97F4A7C15ull + (uint64_t)g,
-                                     300LL * NG * dv);
-      out.anneal_initial += c.first;
-      out.anneal_final += c.second;
-    }
+    for (int g = 0; g < G; g++)
+      for (int part = 0; part < 2; part++) {
+        const int lo = g * NG + (part ? nbound[g] : 0), hi = part ? (g + 1) * NG : g * NG + nbound[g];
+        if (hi - lo < 2) continue;
+        const auto c = anneal_vn_order(out.vn, lo, hi, dv, wb, rb, 0x9E3779B97F4A7C15ull + (uint64_t)(2 * g + part),
+                                       300LL * (hi - lo) * dv);
+        out.anneal_initial += c.first;
+        out.anneal_final += c.second;
+      }
   }
   out.pos.assign(N, 0);
   for (int p = 0; p < N; p++) out.pos[out.vn[p]] = p;

@@ -69,6 +69,7 @@ struct PartitionPlan {
   std::vector<int32_t> rx;  // M, plan order: (x of the row's first cut edge << 8) | mask of its cut
                             // edges by position in the row (0 when none are cut)
   long long anneal_initial = 0, anneal_final = 0;  // VN bank-conflict model cost before / after annealing
+  int interior = 0;  // columns whose edges are all their member's (each member's last run of vn)
   // every member owns rows that receive cut-edge v2c messages from every other
   // member (the tagged exchanges' ordering arguments use it, bp_coop.hip)
   bool all_pairs = false;
