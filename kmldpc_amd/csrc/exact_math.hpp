@@ -29,8 +29,8 @@
 //                FMA ifunc variant (__log_fma).  Used by the soft syndrome
 //                metric (src/kmcodec.cc:155).  Table from tools/gen_log_table.py.
 //   kml_cmul   — std::complex<double> operator* as GCC expands it without
-//                -ffast-math: (ac - bd, ad + bc); the __muldc3 fallback is
-//                reached only when both parts are NaN.
+//                -ffast-math: (ac - bd, ad + bc), and libgcc __muldc3's
+//                recovery of infinities when both parts are NaN.
 //
 // Everything here uses only IEEE-754 basic operations and sqrt, which are
 // correctly rounded on x86-64 and, on gfx950, through kml_div (division;
@@ -43,8 +43,10 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define KML_HD __host__ __device__ __forceinline__
+#define KML_HD_COLD static __host__ __device__ __noinline__
 #else
 #define KML_HD inline
+#define KML_HD_COLD static inline
 #endif
 
 #include <cmath>
@@ -315,6 +317,42 @@ KML_HD double kml_log_t(double x) {
 
 KML_HD double kml_log(double x) { return kml_log_t<true>(x); }
 
-KML_HD cplx kml_cmul(cplx a, cplx b) { return cplx{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+// libgcc __muldc3's Annex G recovery of infinities that the naive product
+// computed as NaN + i NaN (reached only then; out of line: rare)
+KML_HD_COLD cplx kml_cmul_recover(double a, double b, double c, double d) {
+  const double ac = a * c, bd = b * d, ad = a * d, bc = b * c;
+  bool recalc = false;
+  if (std::isinf(a) || std::isinf(b)) {  // the first factor is infinite: box it, NaNs of the other to 0
+    a = copysign(std::isinf(a) ? 1.0 : 0.0, a);
+    b = copysign(std::isinf(b) ? 1.0 : 0.0, b);
+    if (std::isnan(c)) c = copysign(0.0, c);
+    if (std::isnan(d)) d = copysign(0.0, d);
+    recalc = true;
+  }
+  if (std::isinf(c) || std::isinf(d)) {  // the second factor is infinite
+    c = copysign(std::isinf(c) ? 1.0 : 0.0, c);
+    d = copysign(std::isinf(d) ? 1.0 : 0.0, d);
+    if (std::isnan(a)) a = copysign(0.0, a);
+    if (std::isnan(b)) b = copysign(0.0, b);
+    recalc = true;
+  }
+  if (!recalc && (std::isinf(ac) || std::isinf(bd) || std::isinf(ad) || std::isinf(bc))) {  // overflow: NaNs to 0
+    if (std::isnan(a)) a = copysign(0.0, a);
+    if (std::isnan(b)) b = copysign(0.0, b);
+    if (std::isnan(c)) c = copysign(0.0, c);
+    if (std::isnan(d)) d = copysign(0.0, d);
+    recalc = true;
+  }
+  if (!recalc) return cplx{ac - bd, ad + bc};
+  return cplx{INFINITY * (a * c - b * d), INFINITY * (a * d + b * c)};
+}
+
+// std::complex<double> operator* as GCC compiles it without -ffast-math:
+// (ac - bd, ad + bc), and __muldc3 when both parts are NaN.
+KML_HD cplx kml_cmul(cplx a, cplx b) {
+  const double x = a.re * b.re - a.im * b.im, y = a.re * b.im + a.im * b.re;
+  if (std::isnan(x) && std::isnan(y)) return kml_cmul_recover(a.re, a.im, b.re, b.im);
+  return cplx{x, y};
+}
 
 }  // namespace kml

@@ -905,7 +905,10 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
         if (j < S) {
           double g;
           m = member0_margin<KC>(cl, ys[j].x, ys[j].y, g);
-          t = (float)((drift + g * inv2c) * (1.0 - 0x1p-20));  // D + g / (2 Cmax), rounded down
+          // D + g / (2 Cmax), rounded down; past the float range a finite 2^127
+          // (an infinite threshold would never let the word be re-assigned)
+          const double td = (drift + g * inv2c) * (1.0 - 0x1p-20);
+          t = td < 0x1p127 ? (float)td : 0x1p127f;
         }
       };
       auto commit = [&](int q, bool m, float t) {

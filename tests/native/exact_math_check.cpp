@@ -1,5 +1,7 @@
-// Pins kmldpc_amd/csrc/exact_math.hpp against glibc hypot and libgcc __divdc3
-// (the routines the reference calls).  Built and run by tests/test_host.py.
+// Pins kmldpc_amd/csrc/exact_math.hpp against glibc hypot, libgcc __divdc3 and
+// std::complex<double> operator* (inline product + libgcc __muldc3) — the
+// routines the reference calls.  Built and run by tests/test_host.py.
+#include <cmath>
 #include <complex>
 #include <cstdio>
 #include <cstdlib>
@@ -28,6 +30,31 @@ int main(int argc, char** argv) {
                 (q.imag() == r.im || (q.imag() != q.imag() && r.im != r.im));
     if (!same) { if (bad_d < 5) printf("cdiv (%a,%a)/(%a,%a): (%a,%a) vs (%a,%a)\n", a, b, c, d, q.real(), q.imag(), r.re, r.im); bad_d++; }
   }
-  printf("n=%ld hypot_mismatch=%ld cdiv_mismatch=%ld\n", n, bad_h, bad_d);
-  return (bad_h || bad_d) ? 1 : 0;
+  // complex products, with infinities, NaNs, zeros and overflow among the operands
+  const double sp[] = {0.0, -0.0, 1.0, -2.5, 1e300, -1e300, 1e-300, INFINITY, -INFINITY, NAN, -NAN};
+  const int nsp = sizeof(sp) / sizeof(sp[0]);
+  long bad_m = 0, nm = 0;
+  auto same_d = [](double u, double v) {
+    return (u != u && v != v) || (u == v && std::signbit(u) == std::signbit(v));
+  };
+  auto check_mul = [&](double a, double b, double c, double d) {
+    volatile double va = a, vb = b, vc = c, vd = d;  // no constant folding of the library product
+    const std::complex<double> q = std::complex<double>(va, vb) * std::complex<double>(vc, vd);
+    const kml::cplx r = kml::kml_cmul({a, b}, {c, d});
+    ++nm;
+    if (!same_d(q.real(), r.re) || !same_d(q.imag(), r.im)) {
+      if (bad_m < 5) printf("cmul (%a,%a)*(%a,%a): (%a,%a) vs (%a,%a)\n", a, b, c, d, q.real(), q.imag(), r.re, r.im);
+      bad_m++;
+    }
+  };
+  for (int i = 0; i < nsp; i++)
+    for (int j = 0; j < nsp; j++)
+      for (int k = 0; k < nsp; k++)
+        for (int l = 0; l < nsp; l++) check_mul(sp[i], sp[j], sp[k], sp[l]);
+  for (long i = 0; i < n / 4; i++) {
+    const double s = std::exp2(ud(g) * 10);
+    check_mul(nd(g) * s, nd(g), nd(g) * s, nd(g) * (i % 5 == 0 ? 0.0 : 1.0));
+  }
+  printf("n=%ld hypot_mismatch=%ld cdiv_mismatch=%ld cmul_mismatch=%ld (of %ld)\n", n, bad_h, bad_d, bad_m, nm);
+  return (bad_h || bad_d || bad_m) ? 1 : 0;
 }

@@ -155,14 +155,16 @@ def test_host_only_context_refuses_gpu_calls(data_dir):
 
 
 def test_exact_math_host_restatement(tmp_path):
-    """kml_hypot / kml_cdiv (kmldpc_amd/csrc/exact_math.hpp) vs glibc hypot and
-    libgcc __divdc3 — the routines std::abs / operator/ call in the reference."""
+    """kml_hypot / kml_cdiv / kml_cmul (kmldpc_amd/csrc/exact_math.hpp) vs glibc
+    hypot, libgcc __divdc3 and std::complex operator* (+ __muldc3, on every
+    combination of zeros, infinities, NaNs and overflowing parts) — the routines
+    std::abs / operator/ / operator* call in the reference."""
     exe = tmp_path / "emc"
     src = os.path.join(REPO, "tests", "native", "exact_math_check.cpp")
     subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", "-o", str(exe), src], check=True)
     out = subprocess.run([str(exe), "1000000"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
-    assert "hypot_mismatch=0 cdiv_mismatch=0" in out.stdout
+    assert "hypot_mismatch=0 cdiv_mismatch=0 cmul_mismatch=0" in out.stdout
 
 
 def test_exp_host_restatement(tmp_path):
