@@ -120,7 +120,9 @@ int kml_encode(const kml_ctx *ctx, const uint8_t *uu, uint8_t *cc, int B);
  * reference's M2V).  Outputs (any may be NULL): uu_hat[B][K], ret[B] (the
  * reference return value iter + (iter < max_iter)), cc_hat[B][Ncol],
  * syn[B][M] (syndrom_soft; rows are only written when a CN phase runs, like
- * the reference's member array). */
+ * the reference's member array).  iter_count = 0 runs no iteration and, like
+ * the reference (uu_hat is written inside its loop), leaves uu_hat and cc_hat
+ * as the caller passed them. */
 int kml_bp_decode(kml_ctx *ctx, const double *p0, int B, int iter_count, uint8_t *uu_hat, int32_t *ret,
                   uint8_t *cc_hat, double *syn, int flags);
 

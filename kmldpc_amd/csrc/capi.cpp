@@ -1052,9 +1052,14 @@ int kml_bp_decode(kml_ctx *c, const double *p0, int B, int iter_count, uint8_t *
   a.syn = d_syn;
   int slot;
   TRY(run_bp(c, a, slot));
-  TRY(copy_out(c, uu_hat, d_uh, (size_t)B * L.K, flags));
+  // the reference writes uu_hat (and cc_hat_) only inside its iteration loop
+  // (binaryldpccodec.cc:177-216): with iter_count = 0 the kernels write
+  // neither, and the caller's arrays stay as they were
+  if (iter_count > 0) {
+    TRY(copy_out(c, uu_hat, d_uh, (size_t)B * L.K, flags));
+    TRY(copy_out(c, cc_hat, d_cch, (size_t)B * L.N, flags));
+  }
   TRY(copy_out(c, ret, d_ret, (size_t)B, flags));
-  TRY(copy_out(c, cc_hat, d_cch, (size_t)B * L.N, flags));
   TRY(copy_out(c, syn, d_syn, (size_t)B * L.M, flags));
   return sync(c);
 }
