@@ -250,18 +250,20 @@ __global__ void km_final_kernel(const double *__restrict__ cons, const double *_
 
 // ---------------------------------------------------------------------------
 // Fused k-means: one workgroup of two waves per codeword runs the whole
-// KMeans::Run in one launch.  The symbols are staged in LDS once; each
-// iteration assigns in parallel (the screening of km_assign, 64-symbol words by
-// ballot) and then adds the cluster-0 members' values onto the cumulative sums
-// in ascending symbol order — the reference's sequential rounding — with the
-// WORD SCAN below (km_word_sum), and every lane updates hatH.
-// LDS per codeword (km_lds): the symbols 16 S bytes, two buffers of membership
-// words and a drift threshold per word; PEG2304/QPSK 18,648 bytes, so 8
-// codewords share a CU (the 16 KB register budget of 4 waves per SIMD allows 8).
+// KMeans::Run.  The symbols are staged in LDS once; each iteration assigns in
+// parallel (same screening as km_assign, 64-symbol words by ballot), lists the
+// cluster-0 members' indices in ascending symbol order (u16, LDS), and sums
+// their values onto the cumulative sum in that order (the reference's
+// sequential rounding: wave 0 the real chain, wave 1 the imaginary chain, by
+// exact binade-segmented scans, ordered_sum_wave); lane 0 then updates h_hat.
+// y is read from HBM once; LDS per codeword is 16 S + S bytes + 12 per word
+// (km_lds), so 8 codewords share a CU for QPSK/PEG2304 (7 with the full-length
+// member list: 3.65 -> see DESIGN.md).
 //
-// Per-iteration latency bounds this kernel (each codeword is a chain of
-// dependent steps), so the iterations skip the work whose outcome is already
-// known, exactly:
+// Per-iteration latency is what bounds this kernel (each codeword is a chain
+// of dependent steps; a dependent VALU step costs ~40 cycles with 3-4 waves
+// per SIMD), so the iterations skip the work whose outcome is already known,
+// exactly:
 //   * convergence (kmeans.cc:47-56) compares clusters_ = c_k * hatH with the
 //     previous iteration's; lanes k < KC compute both at the iteration START
 //     (the cluster points the assignment needs anyway), so a converged
@@ -277,25 +279,35 @@ __global__ void km_final_kernel(const double *__restrict__ cons, const double *_
 //     the symbol's decision cannot change.  A 64-symbol word is re-assigned
 //     when any of its symbols may have changed: each word keeps the minimum
 //     over its symbols of T = D(ref) + g / (2 Cmax) (float, rounded down);
-//   * the word scan caches each word's summary at the running sum's binade and
-//     recomputes it only when the word's membership or that binade changes;
-//   * the divisions of the update by (cnt, 0) and by c[0] take __divdc3's own
-//     branch with the constant parts hoisted, and share one reciprocal per
-//     divisor (exact: the same operations on the same values).
-constexpr int kFusedT = 128;    // two waves per codeword
+//   * the member list is rebuilt only when some word's membership bits
+//     changed (each wave scans the word popcounts itself and scatters its own
+//     words: no barrier in between);
+//   * the cumulative-mean division by (cnt, 0) and the division by c[0] take
+//     __divdc3's own branch with the constant parts hoisted (exact: same
+//     operations on the same values).
+// Measured (MI355X, 32768 PEG2304/QPSK codewords at Es/N0 2 dB, 19.9
+// iterations each): 4.28 ms -> 3.31 ms; tools/km_stamps.py gives the phases.
+constexpr int kFusedT = 128;  // two waves per codeword (the two sum chains), up to 7 codewords per CU (LDS)
 constexpr int kFusedMaxW = 64;  // 64-symbol words: S <= 4096
-// Dynamic LDS of one codeword: the symbols [S] double2, the membership words
-// [2][Sw] u64 and their drift thresholds [2][Sw] float, both double-buffered
-// by iteration parity (a wave still in iteration i reads buffer i & 1 while
-// the other wave's assignment of i + 1 writes the other one).
+// Dynamic LDS of one codeword: the symbols [S] double2, the compacted member
+// list [cap + 24] u16 (cap = S/2 rounded up to 8: cluster 0 of a constellation
+// of >= 2 points; a larger cluster, seen only on degenerate inputs, is summed
+// straight from the membership words), the membership words [2][Sw] u64 and
+// their drift thresholds [2][Sw] float, both double-buffered by iteration
+// parity (a wave still in iteration i reads buffer i & 1 while the other
+// wave's assignment of i + 1 writes the other one).  PEG2304/QPSK: 20,488
+// bytes + ~120 static, so 8 codewords share a CU (the 16 KB register budget of
+// 4 waves per SIMD allows 8).
 struct KmLds {
-  int off_wbits, off_wthr, bytes;
+  int cap, off_mem, off_wbits, off_wthr, bytes;
 };
 __host__ __device__ constexpr KmLds km_lds(int S) {
+  const int cap = ((S + 1) / 2 + 7) & ~7;
   const int Sw = (S + 63) / 64;
-  const int off_wbits = 16 * S;
+  const int off_mem = 16 * S;
+  const int off_wbits = (off_mem + 2 * (cap + 24) + 7) & ~7;
   const int off_wthr = off_wbits + 16 * Sw;
-  return KmLds{off_wbits, off_wthr, off_wthr + 8 * Sw};
+  return KmLds{cap, off_mem, off_wbits, off_wthr, off_wthr + 8 * Sw};
 }
 
 // Phase timing (stamps build, -DKML_STAMPS=1; tools/km_stamps.py): thread 0's
@@ -303,11 +315,11 @@ __host__ __device__ constexpr KmLds km_lds(int S) {
 #ifndef KML_STAMPS
 #define KML_STAMPS 0
 #endif
-enum { KS_PRO, KS_CLUSTERS, KS_ASSIGN, KS_BARRIER, KS_SUM, KS_ITERS, KS_WORDS, KS_WALKS, KS_CW, KS_UPDATE, KS_ROUNDS,
-       KS_SEQ, KS_SLOTS = 16 };
+enum { KS_PRO, KS_CLUSTERS, KS_ASSIGN, KS_COMPACT, KS_SUM, KS_ITERS, KS_WORDS, KS_COMPACTIONS, KS_CW, KS_UPDATE, KS_STEPS,
+       KS_SLOTS = 16 };
 __device__ unsigned long long kml_km_stamps[KS_SLOTS];
 #if KML_STAMPS
-// accumulated in thread 0's registers, flushed once per workgroup
+// accumulated in thread 0's registers, flushed once per workgroup (KM_FLUSH)
 #define KM_STAMP(i)                                                \
   do {                                                             \
     if (tid == 0) {                                                \
@@ -348,15 +360,13 @@ template <int CTRL, int ROWS>
 __device__ __forceinline__ int dpp_add_step_i(int v) {
   return v + __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, false);
 }
-// inclusive scan over the lanes of each half (HALF) or the whole wave
-template <bool HALF>
-__device__ __forceinline__ int lane_inclusive_scan_i(int v) {
+__device__ __forceinline__ int wave_inclusive_scan_i(int v) {
   v = dpp_add_step_i<0x111, 0xF>(v);  // row_shr:1
   v = dpp_add_step_i<0x112, 0xF>(v);  // row_shr:2
   v = dpp_add_step_i<0x114, 0xF>(v);  // row_shr:4
   v = dpp_add_step_i<0x118, 0xF>(v);  // row_shr:8
   v = dpp_add_step_i<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
-  if constexpr (!HALF) v = dpp_add_step_i<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+  v = dpp_add_step_i<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
   return v;
 }
 __device__ __forceinline__ float wave_min_f(float v) {
@@ -368,27 +378,98 @@ __device__ __forceinline__ float wave_min_f(float v) {
   v = dpp_min_step<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
+
+// acc + y[2 m_0] + y[2 m_1] + ... + y[2 m_(n-1)] in that order (the
+// reference's rounding), m the compacted member indices (u16, 16-byte
+// aligned, at least n + 24 readable; indices past n are clamped into [0, S)).
+// Software pipeline over blocks of 8: the indices of block b + 2 and the
+// values of block b + 1 (from indices already in registers) are in flight
+// while block b is added, so neither LDS latency sits on the chain of
+// dependent adds.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void fetch8(const double *yv, u32x4 q, int S, double (&v)[8]) {
+  const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = yv[2 * min((int)(w[k] & 0xffffu), S - 1)];
+    v[2 * k + 1] = yv[2 * min((int)(w[k] >> 16), S - 1)];
+  }
+}
+__device__ __forceinline__ double ordered_sum(double acc, const double *yv, const unsigned short *m, int n, int S) {
+  // The index list is the same for both lanes; left uniform, hipcc moves the
+  // indices to SGPRs (v_readfirstlane) right after their loads, which waits
+  // for them on the spot.  A VGPR base address keeps them in VGPRs, waited
+  // for only where the values' addresses are formed, a block later.
+  unsigned mb = lds_addr(m);
+  asm volatile("" : "+v"(mb));
+  double cur[8];
+  fetch8(yv, lds_ld<u32x4>(mb), S, cur);
+  u32x4 qn = lds_ld<u32x4>(mb + 16);
+  int i = 0;
+#pragma clang loop unroll(disable)  // unrolled, the second copy waits for the first copy's index load
+  for (; i + 8 <= n; i += 8) {
+    const u32x4 q2 = lds_ld<u32x4>(mb + 2 * i + 32);
+    double nxt[8];
+    fetch8(yv, qn, S, nxt);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc = acc + cur[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
+    qn = q2;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k)  // the tail (< 8 values), already loaded
+    if (i + k < n) acc = acc + cur[k];
+  return acc;
+}
+
+// The same sum computed by a whole wave (binade-segmented integer scans;
+// tools/probe/km_scan_model.py is a CPU model of exactly these steps, checked
+// against the sequential sum on adversarial inputs).  While the running sum
+// stays in one binade [2^(e-1), 2^e) (magnitude; sign sg), every rounded add
+// is a move on the fixed grid u = 2^(e-53): with A = |acc| / u (an integer in
+// [2^52, 2^53)) and X = sg x / u (exact ldexp), RN(acc + x) = sg (A + rint(X)) u
+// unless X is a tie (frac 0.5: the parity of the result decides) or the result
+// leaves the binade.  Each lane takes kScanPer consecutive elements, rounds
+// them to the grid (v_rndne), sums them locally, and a DPP exclusive scan of
+// the lane totals gives every prefix A + P.  All elements before the first one
+// that is large (|X| >= 2^51: keeps every partial sum of valid elements below
+// 2^53, hence exact) or whose prefix leaves [2^52 + 1, 2^53 - 1] (then the
+// exact sum lies inside the binade, where RN is the grid rounding) are exact;
+// that element is added with a real fp64 add and the scan resumes after it.
+// Ties do not stop the scan: they count floor(X), and afterwards, in element
+// order, each tie whose corrected prefix is odd rounds up (ties to even),
+// adding 1 to every later prefix (kScanMargin keeps the range test valid
+// under those corrections).  A zero or non-finite sum, and runs after an
+// early exit, are added one by one.  On MI355X a dependent f64 add chain
+// costs ~40 cycles per element here (LDS index + value loads, other waves on
+// the SIMD); a step costs about 50 dependent instructions.
+// elements per lane per step: 5 covers a QPSK cluster-0 list (~286) in one
+// step; measured per 32768 PEG2304/QPSK codewords: 4 -> 3.42 ms, 5 -> 3.31 ms,
+// 8 -> 3.89 ms (longer in-lane chains and registers)
+#ifndef KML_KM_SCAN_PER
+#define KML_KM_SCAN_PER 5
+#endif
+constexpr int kScanPer = KML_KM_SCAN_PER;
+constexpr double kScanMargin = 64.0;      // grid steps kept from the binade ends: room for the tie corrections
+constexpr int kScanMaxTies = 32;          // ties resolved in one step (each moves later prefixes by <= 1)
 template <int CTRL, int ROWS>
 __device__ __forceinline__ double dpp_add_step(double v) {
   const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWS, 0xF, false);
   const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWS, 0xF, false);
   return v + __hiloint2double(hi, lo);
 }
-// sum over the lanes below this one in its half (HALF) or the wave: a shift
-// by one lane, then the row / broadcast steps (each partial sum covers a
-// contiguous lane range: exact where the prefixes it spans are)
-template <bool HALF>
-__device__ __forceinline__ double lane_exclusive_scan(double v, int lane) {
-  int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xF, 0xF, false);  // wave_shr:1
-  int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xF, 0xF, false);
-  if (HALF && lane == 32) lo = hi = 0;  // the second half starts at zero
+// sum over the lanes below this one (exact where those sums are)
+__device__ __forceinline__ double wave_exclusive_scan(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xF, 0xF, false);  // wave_shr:1
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xF, 0xF, false);
   v = __hiloint2double(hi, lo);
   v = dpp_add_step<0x111, 0xF>(v);  // row_shr:1
   v = dpp_add_step<0x112, 0xF>(v);  // row_shr:2
   v = dpp_add_step<0x114, 0xF>(v);  // row_shr:4
   v = dpp_add_step<0x118, 0xF>(v);  // row_shr:8: prefix within each row of 16
   v = dpp_add_step<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
-  if constexpr (!HALF) v = dpp_add_step<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+  v = dpp_add_step<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
   return v;
 }
 __device__ __forceinline__ double lane_d(double v, int l) {
@@ -399,206 +480,121 @@ __device__ __forceinline__ uint64_t lane_u64(uint64_t v, int l) {
   return ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
          (unsigned)__builtin_amdgcn_readlane((int)v, l);
 }
-
-// ---------------------------------------------------------------------------
-// The word scan (km_word_sum): acc + the cluster-0 members' values in
-// ascending symbol order, with the reference's rounding after every add
-// (kmeans.cc:45, idxSum[0] += data_[j]).  tools/probe/km_word_model.py is a
-// CPU model of exactly these steps, checked against the sequential sum on
-// random, sign-changing, tie-heavy and extreme streams.
-//
-// While the running sum stays in one binade [2^(e-1), 2^e) (sign sg), every
-// rounded add is a move on the grid u = 2^(e-53): with A = |acc| / u (an
-// integer in [2^52, 2^53)) and X = sg x / u (an exact scaling),
-// RN(acc + x) = sg (A + rint(X)) u unless X is a tie (frac 0.5: the parity of
-// the result decides, ties to even) or the result leaves the binade.  So a
-// 64-symbol WORD's members contribute, at binade (e, sg), a grid sum G, local
-// prefixes whose min and max say whether they stay in the binade, and the
-// parities of its ties' local prefixes.  That summary depends only on the
-// word's membership bits and (e, sg): each lane keeps its word's summary in
-// registers and recomputes it (walks the word's members) only when one of
-// them changed, which after the first iterations is rare.  Per round:
-//   1. dirty lanes walk their word (the rest wait);
-//   2. an exclusive lane scan of the G gives each word's starting prefix
-//      A + E (exact: every partial sum up to the first failing word is a
-//      difference of in-range prefixes);
-//   3. the first word whose prefixes may leave [2^52 + 64, 2^53 - 64], that
-//      holds a large element (|X| >= 2^51) or that brings the tie count past
-//      32 FAILS; the words before it are exact;
-//   4. their ties, in order, round up when the corrected prefix is odd (each
-//      adds 1 to every later prefix; the 64-step margin covers 32 ties);
-//   5. acc = sg (A + E(fail) + U) u; the failing word is added element by
-//      element with real fp64 adds, and the next round starts after it at
-//      acc's (new) binade.
-// A zero, non-finite or extreme acc, and a chain whose sum will grow past
-// several binades this iteration (the previous iteration's change exceeded
-// 2|acc|: the first iterations), go word by word with real adds.
-// Lane layout: HALF (Sw <= 32): lane l holds word l & 31 of chain l >> 5 (the
-// real chain in lanes 0-31, the imaginary one in 32-63), so one wave sums
-// both chains; otherwise lane l holds word l of the chain of its wave.
-constexpr double kWordLo = 0x1p52 + 64.0, kWordHi = 0x1p53 - 64.0;
-constexpr int kWordMaxTies = 32;
-constexpr int kWordHard = 1 << 12;  // a word's tie count when it must be added element by element
-
-struct WordCache {
-  uint64_t mask;  // the membership bits the summary was taken for
-  int key;        // its binade and sign, 2 e + (sg < 0); 0x7fffffff = none
-  double G, mn, mx;  // grid sum, min and max local prefix (+inf / -inf: no members)
-  int ntie;       // ties (kWordHard: a large element or more than kWordMaxTies)
-  unsigned tpar;  // bit i: parity of the local prefix at tie i
-};
-
-// parity of an integer-valued double
-__device__ __forceinline__ unsigned dparity(double v) {
-  const double h = v * 0.5;
-  return h != floor(h) ? 1u : 0u;
-}
-
-__device__ __forceinline__ void word_elem(double x, double scale, double &P, double &mn, double &mx, int &nt,
-                                          unsigned &tp, bool &hard) {
-  const double X = x * scale;  // exact: sg x 2^(53-e) (a subnormal product only for |X| << 1)
-  hard = hard || !(fabs(X) < 0x1p51);
-  const double fl = floor(X);
-  const bool tie = (X - fl) == 0.5;
-  P = P + (tie ? fl : rint(X));
-  if (tie) {  // rare
-    if (nt < kWordMaxTies) tp |= dparity(P) << nt;
-    ++nt;
-  }
-  mn = fmin(mn, P);
-  mx = fmax(mx, P);
-}
-
-// the summary of one word (lane-divergent loop over its members, four loads
-// in flight)
-__device__ __forceinline__ void word_walk(const double *yv, int base, uint64_t bits, double scale, WordCache &wc) {
-  double P = 0.0, mn = INFINITY, mx = -INFINITY;
-  int nt = 0;
-  unsigned tp = 0;
-  bool hard = false;
-  while (bits) {
-    int j[4];
+__device__ double ordered_sum_wave(double acc, const double *yv, const unsigned short *m, int n, int S, int lane,
+                                   int &steps) {
+  int i = 0, seq = 0;
+  while (i < n) {  // wave-uniform
+    ++steps;
+    const int c = min(64 * kScanPer, n - i);
+    double x[kScanPer];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      j[k] = bits ? __builtin_ctzll(bits) : -1;
-      bits &= bits - 1;
+    for (int k = 0; k < kScanPer; ++k) {
+      const int j = i + kScanPer * lane + k;
+      x[k] = j < n ? yv[2 * min((int)m[j], S - 1)] : 0.0;
     }
-    double x[4];
+    if (seq > 0 || !(acc != 0.0 && isfinite(acc))) {  // one by one, lane-major element order
+      const int mm = seq > 0 ? min(seq, c) : 1;
+      for (int l = 0; l * kScanPer < mm; ++l) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = yv[2 * (base + max(j[k], 0))];
+        for (int k = 0; k < kScanPer; ++k)
+          if (l * kScanPer + k < mm) acc = acc + lane_d(x[k], l);
+      }
+      seq = seq > 0 ? seq - mm : 0;
+      i += mm;
+      continue;
+    }
+    const int e = __builtin_amdgcn_frexp_exp(acc);  // |acc| in [2^(e-1), 2^e)
+    const double sg = acc < 0.0 ? -1.0 : 1.0;
+    const double A = __builtin_amdgcn_ldexp(fabs(acc), 53 - e);
+    double T[kScanPer];
+    unsigned bigm = 0, tiem = 0;
+    double run = 0.0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (j[k] >= 0) word_elem(x[k], scale, P, mn, mx, nt, tp, hard);
-  }
-  wc.G = P;
-  wc.mn = mn;
-  wc.mx = mx;
-  wc.ntie = (hard || nt > kWordMaxTies) ? kWordHard : nt;
-  wc.tpar = tp;
-}
-
-__device__ __forceinline__ bool word_scan_ok(double acc) { return fabs(acc) >= 0x1p-960 && fabs(acc) < INFINITY; }
-
-// acc: this lane's chain's running sum (uniform over the chain's lanes);
-// mask: the lane's word's membership bits; comp: the lane's chain (0 real,
-// 1 imaginary); seq: the chain goes word by word this iteration.
-template <bool HALF>
-__device__ double km_word_sum(double acc, const double2 *ys, uint64_t mask, int S, int Sw, int lane, int comp, bool seq,
-                              WordCache &wc, int &rounds, int &walks) {
-  const int w = HALF ? (lane & 31) : lane;
-  const bool inw = w < Sw;
-  const double *yv = reinterpret_cast<const double *>(ys) + comp;
-  int w0 = 0;
-  for (;;) {
-    const bool pend = w0 < Sw;
-    if (!__ballot(pend)) break;
-    ++rounds;
-    const bool ok = pend && !seq && word_scan_ok(acc);
-    int wf = pend ? w0 : Sw;  // the word added element by element (Sw: none)
-    if (__ballot(ok)) {
-      const int e = __builtin_amdgcn_frexp_exp(acc);  // |acc| in [2^(e-1), 2^e)
-      const double sg = acc < 0.0 ? -1.0 : 1.0;
-      const double A = __builtin_amdgcn_ldexp(fabs(acc), 53 - e);
-      const double scale = __builtin_amdgcn_ldexp(sg, 53 - e), iscale = __builtin_amdgcn_ldexp(sg, e - 53);
-      const int key = 2 * e + (acc < 0.0 ? 1 : 0);
-      const bool act = ok && inw && w >= w0;
-      const bool dirty = act && (mask != wc.mask || key != wc.key);
-      if (__ballot(dirty)) {
-        walks += __popcll(__ballot(dirty));
-        if (dirty) {
-          word_walk(yv, 64 * w, mask, scale, wc);
-          wc.mask = mask;
-          wc.key = key;
-        }
-      }
-      const double g = act ? wc.G : 0.0;
-      const double E = lane_exclusive_scan<HALF>(g, lane);
-      const int nti = lane_inclusive_scan_i<HALF>(act ? wc.ntie : 0);
-      const bool fail = act && (nti > kWordMaxTies || !(A + E + wc.mn >= kWordLo) || !(A + E + wc.mx <= kWordHi));
-      const uint64_t fb = __ballot(fail);
-      // this chain's first failing word
-      const uint64_t fc = HALF ? (lane < 32 ? (fb & 0xFFFFFFFFull) : (fb >> 32)) : fb;
-      if (ok) wf = fc ? __builtin_ctzll(fc) : Sw;
-      // the ties of the words before it, in order (rare)
-      const bool tl = act && w < wf && wc.ntie > 0;
-      uint64_t tb = __ballot(tl);
-      int U0 = 0, U1 = 0;
-      if (tb) {
-        const uint64_t qb = __ballot(tl && dparity(A + E));
-        while (tb) {
-          const int l = __builtin_ctzll(tb);
-          tb &= tb - 1;
-          const int nt = __builtin_amdgcn_readlane(wc.ntie, l);
-          const unsigned tp = (unsigned)__builtin_amdgcn_readlane((int)wc.tpar, l);
-          const unsigned q = (unsigned)(qb >> l) & 1u;
-          int &U = (HALF && l >= 32) ? U1 : U0;
-          for (int i = 0; i < nt; ++i) U += (int)(q ^ ((tp >> i) & 1u) ^ ((unsigned)U & 1u));
-        }
-      }
-      // the prefix before word wf (all of the chain's words when wf = Sw)
-      const double sel = (w == wf) ? E : E + g;
-      const int wf0 = __builtin_amdgcn_readlane(wf, 0);
-      double T = lane_d(sel, min(wf0, Sw - 1));
-      int U = U0;
-      if (HALF) {
-        const int wf1 = __builtin_amdgcn_readlane(wf, 32);
-        const double T1 = lane_d(sel, 32 + min(wf1, Sw - 1));
-        if (lane >= 32) {
-          T = T1;
-          U = U1;
-        }
-      }
-      if (ok) acc = (A + T + (double)U) * iscale;  // exact: an integer < 2^53 times a power of two, normal
+    for (int k = 0; k < kScanPer; ++k) {
+      const double X = __builtin_amdgcn_ldexp(sg * x[k], 53 - e);
+      const double fl = floor(X);
+      const bool big = !(fabs(X) < 0x1p51);
+      const bool tie = !big && (X - fl) == 0.5;
+      bigm |= (big ? 1u : 0u) << k;
+      tiem |= (tie ? 1u : 0u) << k;
+      // a tie counts its lower neighbour; the parity pass below adds 1 where it rounds up
+      run = run + (big ? 0.0 : (tie ? fl : rint(X)));
+      T[k] = run;
     }
-    // the failing word (or, going word by word, word w0), element by element
-    const int f0 = __builtin_amdgcn_readlane(wf, 0);
-    const int f1 = HALF ? __builtin_amdgcn_readlane(wf, 32) : Sw;
-    if (f0 < Sw || f1 < Sw) {
-      // chain 0: the real component (HALF) or the wave's; chain 1: the imaginary one
-      const double *y0 = HALF ? reinterpret_cast<const double *>(ys) : yv;
-      const double *y1 = reinterpret_cast<const double *>(ys) + 1;
-      const uint64_t m0 = f0 < Sw ? lane_u64(mask, f0) : 0ull;
-      const uint64_t m1 = (HALF && f1 < Sw) ? lane_u64(mask, 32 + f1) : 0ull;
-      const double x0 = y0[2 * min(64 * (f0 < Sw ? f0 : 0) + lane, S - 1)];
-      double x1 = 0.0;
-      if (HALF) x1 = y1[2 * min(64 * (f1 < Sw ? f1 : 0) + lane, S - 1)];
-      double a0 = lane_d(acc, 0), a1 = HALF ? lane_d(acc, 32) : 0.0;
-      uint64_t r0 = m0, r1 = m1;
-      while (r0 | r1) {  // wave-uniform
-        if (r0) {
-          const int b = __builtin_ctzll(r0);
-          r0 &= r0 - 1;
-          a0 = a0 + lane_d(x0, b);
-        }
-        if (r1) {
-          const int b = __builtin_ctzll(r1);
-          r1 &= r1 - 1;
-          a1 = a1 + lane_d(x1, b);
-        }
-      }
-      acc = (HALF && lane >= 32) ? a1 : a0;
+    const double E = wave_exclusive_scan(run);
+    const int kl = min(max(c - kScanPer * lane, 0), kScanPer);  // this lane's elements
+    const int pos0 = kScanPer * lane;                           // their positions in the step
+    unsigned hardm = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      T[k] = A + (E + T[k]);
+      const bool hard = k < kl && (((bigm >> k) & 1u) || !(T[k] >= 0x1p52 + kScanMargin && T[k] <= 0x1p53 - kScanMargin));
+      hardm |= (hard ? 1u : 0u) << k;
     }
-    w0 = wf < Sw ? wf + 1 : Sw;
+    int fh = c;  // the first element that must be added for real
+    {
+      const uint64_t hb = __ballot(hardm != 0);
+      if (hb) {
+        const int lf = __builtin_ctzll(hb);
+        fh = kScanPer * lf + __builtin_amdgcn_readlane(__builtin_ctz(hardm | (1u << kScanPer)), lf);
+      }
+    }
+    // ties before fh, in order: round half to even on the corrected prefix
+    {
+      unsigned tm = 0;
+#pragma unroll
+      for (int k = 0; k < kScanPer; ++k)
+        if (pos0 + k < fh) tm |= tiem & (1u << k);
+      int nt = 0;
+      for (uint64_t tb = __ballot(tm != 0); tb; tb = __ballot(tm != 0)) {  // wave-uniform
+        const int lt = __builtin_ctzll(tb);
+        const int kt = __builtin_ctz((unsigned)__builtin_amdgcn_readlane((int)tm, lt));
+        const int q = kScanPer * lt + kt;
+        if (nt == kScanMaxTies) {  // too many ties for the margin: this one is added for real
+          fh = q;
+          break;
+        }
+        ++nt;
+        double ts = T[0];
+#pragma unroll
+        for (int k = 1; k < kScanPer; ++k)
+          if (kt == k) ts = T[k];
+        const double Tq = lane_d(ts, lt);
+        if ((long long)Tq & 1) {  // odd: the tie rounds up, and so does every later prefix
+#pragma unroll
+          for (int k = 0; k < kScanPer; ++k)
+            if (pos0 + k >= q) T[k] += 1.0;
+        }
+        if (lane == lt) tm &= ~(1u << kt);
+      }
+    }
+    if (fh == c) {
+      const int kk = (c - 1) % kScanPer;
+      double Tl = T[0];
+#pragma unroll
+      for (int k = 1; k < kScanPer; ++k)
+        if (kk == k) Tl = T[k];
+      acc = sg * __builtin_amdgcn_ldexp(lane_d(Tl, (c - 1) / kScanPer), e - 53);
+      i += c;
+    } else {
+      const int lf = fh / kScanPer, fk = fh % kScanPer;
+      double Tpre = T[0], xf = x[0];
+#pragma unroll
+      for (int k = 1; k < kScanPer; ++k) {
+        if (fk == k) xf = x[k];
+        if (fk - 1 == k) Tpre = T[k];
+      }
+      // the prefix before fh: the previous element's (in this lane or the lane below), or A
+      double Tp = fk > 0 ? lane_d(Tpre, lf) : A;
+      if (fk == 0 && lf > 0) {
+        double Tlast = T[kScanPer - 1];
+        Tp = lane_d(Tlast, lf - 1);
+      }
+      acc = sg * __builtin_amdgcn_ldexp(Tp, e - 53);
+      acc = acc + lane_d(xf, lf);  // the exiting / large element, rounded for real
+      i += fh + 1;
+      if (fh < 16) seq = 32;  // exits close together: a short one-by-one run
+    }
   }
   return acc;
 }
@@ -719,27 +715,34 @@ __device__ __forceinline__ cplx cdiv_const(cplx n, cplx dd, const CdivConst &k) 
   return cplx{x, y};
 }
 
-// four waves per SIMD (<= 128 registers): 8 codewords per CU fit the LDS
-template <int KC, bool HALF>
-__global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8 ? 1 : 4))) void km_fused_kernel(
-    const double *__restrict__ cons, const double *__restrict__ rot, const double2 *__restrict__ y, int S, int iters,
-    double2 *__restrict__ h_hat, double2 *__restrict__ h4, double2 *__restrict__ hat_out, int incremental, int bal) {
+// four waves per SIMD (<= 128 registers): 7 codewords per CU fit the LDS, and
+// at 129+ registers only 6 do (QPSK: 3.3 -> 4.1 ms when the exact division's
+// registers pushed it past)
+template <int KC>
+__global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8 ? 1 : 4))) void km_fused_kernel(const double *__restrict__ cons,
+                                                           const double *__restrict__ rot,
+                                                           const double2 *__restrict__ y, int S, int iters,
+                                                           double2 *__restrict__ h_hat, double2 *__restrict__ h4,
+                                                           double2 *__restrict__ hat_out, int incremental, int scan, int bal) {
   extern __shared__ __attribute__((aligned(16))) unsigned char kmem[];
   const KmLds L = km_lds(S);
   double2 *ys = reinterpret_cast<double2 *>(kmem);  // [S] symbols
+  // compacted cluster-0 member indices, ascending: [cap + 24], 16-byte aligned
+  unsigned short *mem = reinterpret_cast<unsigned short *>(kmem + L.off_mem);
   uint64_t *wbits = reinterpret_cast<uint64_t *>(kmem + L.off_wbits);  // [2][Sw] membership words
   float *wthr = reinterpret_cast<float *>(kmem + L.off_wthr);  // [2][Sw] per word: min over its symbols of D(ref) + g / (2 Cmax)
   __shared__ double2 clw[kFusedT / 64][KC];  // each wave's own copy of the clusters (no barrier)
   __shared__ double red_d[kFusedT / 64];
   __shared__ int red_i[kFusedT / 64];
   __shared__ int s_exact;
+  __shared__ int s_flag[1 + kFusedT / 64];  // converged; per wave: member bits changed
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = kFusedT / 64;
   const int cw = blockIdx.x;
   const int Sw = (S + 63) / 64;
 #if KML_STAMPS
   unsigned long long km_prev = __builtin_amdgcn_s_memtime();
-  unsigned long long km_acc[KS_SLOTS] = {};
+  unsigned long long km_acc[KS_STEPS + 1] = {};
   KM_COUNT(KS_CW, 1);
 #endif
   const double2 *yy = y + (long long)cw * S;
@@ -818,19 +821,9 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
   cplx prevk{0.0, 0.0};
   cplx hprev = hat;
   double drift = 0.0;  // D: the same value in every thread
-  // the cumulative cluster-0 sums (kmeans.cc:33-34, 46): this lane's chain's
-  // (HALF: lanes 0-31 real, 32-63 imaginary; else the wave's chain)
-  const int comp = HALF ? (lane >> 5) : wave;
-  double acc = 0.0;
-  double delta = INFINITY;  // the chain's change in the previous iteration
-  WordCache wc;
-  wc.mask = 0;
-  wc.key = 0x7fffffff;
-  wc.G = wc.mn = wc.mx = 0.0;
-  wc.ntie = 0;
-  wc.tpar = 0;
+  double sr = 0.0, si = 0.0;  // cumulative cluster-0 sum (kmeans.cc:33-34, 46)
   int cnt = 0;
-  int rounds = 0, walks = 0;
+  int nmem = 0;  // members in the current list
   KM_STAMP(KS_PRO);
   for (int it = 0; it < iters; ++it) {
     // clusters_[k] = c[k] * hatH, and the convergence test against
@@ -867,16 +860,19 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
     // assignment: is cluster 0 the first minimum?  (kmeans.cc:36-46), only
     // the words whose decisions the drift may have changed; the others keep
     // the previous iteration's bits and thresholds
+    int chg = 0;
     {
       uint64_t need;  // this wave's flagged words (bal: bit = word; else bit q = word wave + NW q)
+      uint64_t oldb;  // lane l: the previous bits of word l (bal) or of word wave + NW l
       if (bal) {
         // both waves test every word (lane = word) and take the flagged words
         // by rank: wave v the ranks v, v + NW, ... (balanced whatever their
         // indices); unflagged words are copied by their index's wave
         const bool inw = lane < Sw;
+        oldb = inw ? prv[lane] : 0ull;
         const bool nd = inw && (!incremental || !(drift < (double)tprv[lane]));
         if (inw && !nd && lane % NW == wave) {
-          cur[lane] = prv[lane];
+          cur[lane] = oldb;
           tcur[lane] = tprv[lane];
         }
         need = 0;
@@ -888,9 +884,10 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
         const int nq = (Sw - wave + NW - 1) / NW;  // <= 64 (S <= 4096)
         const int wl = wave + NW * lane;
         const bool own = lane < nq;
+        oldb = own ? prv[wl] : 0ull;
         const bool needq = own && (!incremental || !(drift < (double)tprv[wl]));
         if (own && !needq) {
-          cur[wl] = prv[wl];
+          cur[wl] = oldb;
           tcur[wl] = tprv[wl];
         }
         need = __ballot(needq);
@@ -914,6 +911,7 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
       auto commit = [&](int q, bool m, float t) {
         const int w = widx(q);
         const uint64_t bits = __ballot(m);
+        if (it == 0 || bits != lane_u64(oldb, q)) chg = 1;
         if (lane == 0) {
           cur[w] = bits;
           tcur[w] = t;
@@ -944,47 +942,70 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
 #endif
       }
     }
+    if (lane == 0) s_flag[1 + wave] = chg;
+    __syncthreads();
+    int rebuild = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) rebuild |= s_flag[1 + w];
     KM_STAMP(KS_ASSIGN);
-    __syncthreads();  // the membership words of this iteration, both waves'
-    KM_STAMP(KS_BARRIER);
-    // the members: cumulative count (kmeans.cc:44) and sums (kmeans.cc:45)
-    const int w = HALF ? (lane & 31) : lane;
-    const uint64_t mask = w < Sw ? cur[w] : 0ull;
-    const int nsc = lane_inclusive_scan_i<HALF>(__popcll(mask));
-    cnt += __builtin_amdgcn_readlane(nsc, HALF ? 31 : 63);
-    const DdRcp yc = dd_rcp((double)cnt);  // the update's divisor, ahead of the sums
-    {
-      [[maybe_unused]] const int r0 = rounds;
-      const double a0 = acc;
-      acc = km_word_sum<HALF>(acc, ys, mask, S, Sw, lane, comp, !(fabs(a0) > 0.5 * delta), wc, rounds, walks);
-      delta = fabs(acc - a0);
-      KM_COUNT(KS_ROUNDS, rounds - r0);
-    }
-    double sr, si;
-    if constexpr (HALF) {
-      sr = lane_d(acc, 0);
-      si = lane_d(acc, 32);
-    } else {  // one chain per wave: exchange through LDS
-      if (lane == 0) red_d[wave] = acc;
+    if (rebuild) {  // member list changed: rebuild it
+      KM_COUNT(KS_COMPACTIONS, 1);
+      // every wave computes the word offsets itself (exclusive prefix of the
+      // popcounts, DPP scan over lanes = words, Sw <= 64) and scatters its own
+      // words' members: no barrier between the two
+      const uint64_t bl = lane < Sw ? cur[lane] : 0ull;
+      const int c = __popcll(bl);
+      const int incl = wave_inclusive_scan_i(c);
+      const int excl = incl - c;
+      nmem = __builtin_amdgcn_readlane(incl, 63);
+      for (int w = wave; w < Sw; w += NW) {
+        const uint64_t bits = ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(bl >> 32), w) << 32) |
+                              (unsigned)__builtin_amdgcn_readlane((int)bl, w);
+        if ((bits >> lane) & 1) {
+          const int p = __builtin_amdgcn_readlane(excl, w) + __popcll(bits & ((1ull << lane) - 1));
+          if (p < L.cap) mem[p] = (unsigned short)(w * 64 + lane);
+        }
+      }
       __syncthreads();
-      sr = red_d[0];
-      si = red_d[1];
-      __syncthreads();  // red_d is reused by the next iteration's exchange
     }
+    KM_STAMP(KS_COMPACT);
+    const int n = nmem;
+    cnt += n;
+    const DdRcp yc = dd_rcp((double)cnt);  // the update's divisor, ahead of the sums
+    if (n > L.cap) {  // more members than the list holds (degenerate input): straight from the words
+      if (tid < 2) {  // lane 0: real chain, lane 1: imaginary chain, ascending j
+        double acc = tid == 0 ? sr : si;
+        const double *yv = reinterpret_cast<const double *>(ys) + tid;
+        for (int w = 0; w < Sw; ++w)
+          for (uint64_t b = cur[w]; b; b &= b - 1) acc = acc + yv[2 * (w * 64 + __builtin_ctzll(b))];
+        red_d[tid] = acc;
+      }
+    } else if (scan) {  // wave 0: the real chain, wave 1: the imaginary chain (kFusedT = 128)
+      int steps = 0;
+      const double acc = ordered_sum_wave(wave == 0 ? sr : si, reinterpret_cast<const double *>(ys) + wave, mem, n, S,
+                                          lane, steps);
+      KM_COUNT(KS_STEPS, steps);
+      if (lane == 0) red_d[wave] = acc;
+    } else if (tid < 2) {  // lane 0: real chain, lane 1: imaginary chain, ascending j
+      red_d[tid] = ordered_sum(tid == 0 ? sr : si, reinterpret_cast<const double *>(ys) + tid, mem, n, S);
+    }
+    __syncthreads();
+    sr = red_d[0];
+    si = red_d[1];
     KM_STAMP(KS_SUM);
     // every lane of both waves updates hatH (the same operations on the same
     // values, kmeans.cc:59-71): no broadcast, no barrier
     {
       const cplx m0 = cdiv_count(sr, si, cnt, yc);  // kmeans.cc:59-62
-      hat = cdiv_const(m0, c0, c0k);               // kmeans.cc:64-71
+      const cplx nh = cdiv_const(m0, c0, c0k);  // kmeans.cc:64-71
+      hat = nh;
     }
     KM_STAMP(KS_UPDATE);
   }
 #if KML_STAMPS
   if (tid == 0) {
     km_acc[KS_WORDS] *= NW;
-    km_acc[KS_WALKS] += walks;
-    for (int i = 0; i < KS_SLOTS; ++i) atomicAdd(&kml_km_stamps[i], km_acc[i]);
+    for (int i = 0; i <= KS_STEPS; ++i) atomicAdd(&kml_km_stamps[i], km_acc[i]);
   }
 #endif
   if (tid == 0) {
@@ -1005,21 +1026,16 @@ bool run_kmeans_fused(const double *cons, const double *rot, const double2 *y, i
   if (S > 64 * kFusedMaxW || lds > 128 * 1024) return false;
   if (const char *e = getenv("KML_KMEANS"))
     if (e[0] == 's') return false;  // KML_KMEANS=split: the two-launch form (A/B)
+  err = hipFuncSetAttribute((const void *)km_fused_kernel<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return true;
   int incremental = 1;  // KML_KM_INCR=0: assign every word every iteration (A/B)
   if (const char *e = getenv("KML_KM_INCR")) incremental = e[0] != '0';
+  int scan = 1;  // KML_KM_SCAN=0: the two-lane sequential sums (A/B)
+  if (const char *e = getenv("KML_KM_SCAN")) scan = e[0] != '0';
   int bal = 1;  // KML_KM_BAL=0: each wave assigns its own words (w % 2) instead of the flagged words by rank (A/B)
   if (const char *e = getenv("KML_KM_BAL")) bal = e[0] != '0';
-  bool half = S <= 32 * 64;  // both chains in one wave (KML_KM_HALF=0: one chain per wave, A/B)
-  if (const char *e = getenv("KML_KM_HALF")) half = half && e[0] != '0';
-  const void *kern = half ? (const void *)km_fused_kernel<KC, true> : (const void *)km_fused_kernel<KC, false>;
-  err = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (err != hipSuccess) return true;
-  if (half)
-    hipLaunchKernelGGL((km_fused_kernel<KC, true>), dim3(B), dim3(kFusedT), lds, s, cons, rot, y, S, iters, h_hat, h4,
-                       hat_out, incremental, bal);
-  else
-    hipLaunchKernelGGL((km_fused_kernel<KC, false>), dim3(B), dim3(kFusedT), lds, s, cons, rot, y, S, iters, h_hat, h4,
-                       hat_out, incremental, bal);
+  hipLaunchKernelGGL(km_fused_kernel<KC>, dim3(B), dim3(kFusedT), lds, s, cons, rot, y, S, iters, h_hat, h4, hat_out,
+                     incremental, scan, bal);
   err = hipGetLastError();
   return true;
 }

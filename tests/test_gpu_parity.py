@@ -453,19 +453,19 @@ def test_kmeans_adversarial_ties(data_dir, modem):
         assert np.array_equal(hh[b], ref, equal_nan=True), b
 
 
-@pytest.mark.parametrize("mode", ["default", "one_chain_per_wave", "owned_words"])
+@pytest.mark.parametrize("mode", ["default", "sequential_sum", "owned_words"])
 @pytest.mark.parametrize("modem", ["2bits_QPSK.txt", "4bit_16QAM_Gray.txt", "6bits_64QAM_Gray.txt"])
-def test_kmeans_word_scan_adversarial(data_dir, modem, mode, monkeypatch):
-    """The fused k-means' word scan (kmeans.hip km_word_sum: per-word grid sums
-    cached across iterations, tie parities, binade exits) against the
-    oracle's sequential cumulative sums (kmeans.cc:33-46), on inputs built to
-    hit its corner cases: noise on a coarse dyadic grid (ties in nearly every
-    word), a cluster-0 centre on an axis (sums that change sign), tiny and huge
-    channels (extreme binades), NaN / inf symbols and realistic frames; both
-    lane layouts (KML_KM_HALF=1: both chains in one wave, 0: one per wave) and
-    both splits of the assignment (KML_KM_BAL=1: flagged words by rank, 0: each
-    wave its own words)."""
-    monkeypatch.setenv("KML_KM_HALF", "0" if mode == "one_chain_per_wave" else "1")
+def test_kmeans_cumulative_sum_adversarial(data_dir, modem, mode, monkeypatch):
+    """The fused k-means' cumulative cluster-0 sums (kmeans.hip
+    ordered_sum_wave: binade-segmented grid scans, tie parities, binade exits)
+    and its incremental assignment against the oracle's sequential
+    kmeans.cc:33-46, on inputs built to hit their corner cases: noise on a
+    coarse dyadic grid (ties), a cluster-0 centre on an axis (sums that change
+    sign), tiny and huge channels (extreme binades; thresholds past the float
+    range), NaN / inf symbols (the complex products' infinity recovery) and
+    realistic frames; with the default kernel, the two-lane sequential sums
+    (KML_KM_SCAN=0) and each wave assigning its own words (KML_KM_BAL=0)."""
+    monkeypatch.setenv("KML_KM_SCAN", "0" if mode == "sequential_sum" else "1")
     monkeypatch.setenv("KML_KM_BAL", "0" if mode == "owned_words" else "1")
     matrix = "PEG8064regular0.5.txt" if "64QAM" in modem else "PEG2304regular0.5.txt"
     ctx = ctx_for(data_dir, matrix, modem, False)

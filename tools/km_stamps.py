@@ -20,7 +20,7 @@ sys.path.insert(0, REPO)
 os.environ.setdefault("KML_LIB", os.path.join(REPO, "kmldpc_amd", "libkmldpc_amd_stamps.so"))
 import kmldpc_amd as K  # noqa: E402
 
-NAMES = ["prologue (load + first max)", "clusters + convergence", "assignment", "barrier", "sum", "update"]
+NAMES = ["prologue (load + first max)", "clusters + convergence", "assignment", "compaction", "sum", "update + barrier"]
 SLOT = [0, 1, 2, 3, 4, 9]
 
 
@@ -44,15 +44,15 @@ def main():
     ctx.sim_decode(snr, blind=True)
     fn(buf.ctypes.data, 0)
     st = buf.astype(np.float64)
-    ncw, iters, words, walks = st[8], st[5], st[6], st[7]
+    ncw, iters, words, comp = st[8], st[5], st[6], st[7]
     sw = (ctx.S + 63) // 64
     print(f"{matrix} + {modem}, snr {snr}: {int(ncw)} codewords, {iters / ncw:.2f} iterations per codeword")
-    print(f"  words assigned per iteration {words / iters:.2f} of {sw}; word walks per iteration (wave 0) {walks / iters:.2f}")
+    print(f"  words assigned per iteration {words / iters:.2f} of {sw}; compactions per iteration {comp / iters:.3f}")
     tot = st[SLOT].sum() / ncw
     for n, i in zip(NAMES, SLOT):
         print(f"  {n:30s} {st[i] / ncw:9.0f} cycles/cw  {st[i] / max(iters, 1):7.0f} /iter  {100 * st[i] / ncw / tot:5.1f}%")
     print(f"  {'total':30s} {tot:9.0f} cycles/cw")
-    print(f"  word-scan rounds per iteration (wave 0) {st[10] / max(iters, 1):.2f}")
+    print(f"  wave-sum steps per iteration (real chain) {st[10] / max(iters, 1):.2f}")
 
 
 if __name__ == "__main__":
