@@ -506,16 +506,6 @@ __device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, 
 #ifndef KML_PART_VN_AGE_PRIO
 #define KML_PART_VN_AGE_PRIO 0
 #endif
-// KML_PART_SPLIT = 1: the VN phase of the last column round runs in two
-// parts.  The interior columns (every edge's row the member's own; the planner
-// puts them last, layout.cpp) need no received c2v: they run right after the
-// CN phase's closing barrier, while the partners' cut-edge c2v are still in
-// flight; the c2v receive follows, then a barrier, then the boundary columns.
-// One barrier more per iteration (after the CN phase) for ~a quarter of the VN
-// work overlapping the receive.
-#ifndef KML_PART_SPLIT
-#define KML_PART_SPLIT 0
-#endif
 constexpr unsigned kTagHi = 0x80000000u;  // bit 63 of a message word (hi dword bit 31)
 constexpr unsigned kHdHi = 0x40000000u;   // bit 62: hard decision (v2c first word)
 
@@ -626,7 +616,7 @@ __device__ __forceinline__ int part_iterations_tagged(
     const int (&vaddr)[RV][3],
     const bool (&vact)[RV], const double (&pv)[RV], const int (&crow)[RC],
     const int (&cbase)[RC], const int (&crx)[RC], const int (&cwb)[RC], const bool (&cact)[RC], const int (&xr)[RX],
-    const int (&xc)[RX], bool vint,
+    const int (&xc)[RX],
     int odd, int &iter_out, bool &conv_out, int &pcnt_out, int &decbuf_out, bool sus0 = false) {
   constexpr int DV = 3, DC = 6, H = 3, NW = T / 64;
   const int tid = threadIdx.x;
@@ -670,22 +660,11 @@ __device__ __forceinline__ int part_iterations_tagged(
 #else
       __builtin_amdgcn_s_setprio(3);
 #endif
-      // KML_PART_SPLIT: pass 0 the interior columns of the last round, then the
-      // c2v receive and a barrier, pass 1 every other column
-      const int npass = (KML_PART_SPLIT && iter > 0) ? 2 : 1;
-#pragma clang loop unroll(disable)
-      for (int pass = 0; pass < npass; ++pass) {
-      if (npass == 2 && pass == 1) {  // the previous CN phase's cut-edge c2v (tag of g - 1) into the mirror slots
-        if (!poll_entries<RX, 1>(xc, tb, tb_c2v, smem, tag ^ 1u, abort)) *sdead = 1;
-        __syncthreads();
-        if (*sdead) return -1;
-      }
       // one column's chains at a time (column-major): the FAST divisions'
       // proofs keep a normalisation's operands live, and interleaving the RV
       // columns step by step doubled the live set (scratch spills in the loop)
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
-        if (npass == 2 && ((r == RV - 1 && vint) != (pass == 0))) continue;
         double c0c[DV];  // the column's c2v, loaded per column (registers)
 #pragma unroll
         for (int k = 0; k < DV; ++k) c0c[k] = *reinterpret_cast<const double *>(smem + vaddr_c2v(vaddr[r][k]));
@@ -735,7 +714,6 @@ __device__ __forceinline__ int part_iterations_tagged(
           }
         }
       }
-      }  // pass
       __builtin_amdgcn_s_setprio(0);
     }
     KML_STAMP(2);
@@ -914,8 +892,7 @@ __device__ __forceinline__ int part_iterations_tagged(
 #endif
     KML_STAMP(7);
     // --------------------------------------- receive c2v of the cut edges
-    // (KML_PART_SPLIT: at the top of the next iteration, after its interior columns)
-    if (!KML_PART_SPLIT && iter + 1 < a.iter_count)
+    if (iter + 1 < a.iter_count)
       if (!poll_entries<RX, 1>(xc, tb, tb_c2v, smem, tag, abort)) *sdead = 1;
     __syncthreads();
 #if KML_PART_FLAG_LATE
@@ -988,10 +965,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
       vaddr[r][k] = ((vx >= 0 ? vx : kMbOob) << 17) | (2 * sl + (vact[r] ? part_c2v_half(sl, EG, DC) : 1));
     }
   }
-  // the last round's column is interior (every edge a row slot: no received c2v)
-  bool vint = vact[RV - 1];
-#pragma unroll
-  for (int k = 0; k < DV; ++k) vint = vint && (vaddr[RV - 1][k] >> 17) == kMbOob;
   int crow[RC], cbase[RC], crx[RC], cwb[RC];
   bool cact[RC];
 #pragma unroll
@@ -1083,7 +1056,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
       }
       const int st = part_iterations_tagged<kG, T, RV, RC, RX, SYN>(a, c.M, cw, gs, g, &sfail, &sdead, member, abort,
                                                                    smem, dec, NG, tb, tb_c2v, vaddr, vact, pv, crow,
-                                                                   cbase, crx, cwb, cact, xr, xc, vint, odd, iter, conv, pcnt,
+                                                                   cbase, crx, cwb, cact, xr, xc, odd, iter, conv, pcnt,
                                                                    decbuf, (fast_allowed & 2) != 0);
       if (st < 0) return;
       if (st == 1) {  // an unproven quotient: redone by the exact launch (every member took this branch)

@@ -451,6 +451,9 @@ __device__ __forceinline__ double ordered_sum(double acc, const double *yv, cons
 #define KML_KM_SCAN_PER 5
 #endif
 constexpr int kScanPer = KML_KM_SCAN_PER;
+#ifndef KML_KM_GROUP  // (A/B) one-wave kernel: flagged words per assignment pass
+#define KML_KM_GROUP 2
+#endif
 constexpr double kScanMargin = 64.0;      // grid steps kept from the binade ends: room for the tie corrections
 constexpr int kScanMaxTies = 32;          // ties resolved in one step (each moves later prefixes by <= 1)
 template <int CTRL, int ROWS>
@@ -480,8 +483,130 @@ __device__ __forceinline__ uint64_t lane_u64(uint64_t v, int l) {
   return ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
          (unsigned)__builtin_amdgcn_readlane((int)v, l);
 }
-__device__ double ordered_sum_wave(double acc, const double *yv, const unsigned short *m, int n, int S, int lane,
-                                   int &steps) {
+// One step of the scan, split in two phases so that a wave can run the real
+// and the imaginary chain side by side: scan_a is straight-line (grid values,
+// the lane totals' DPP scan, the prefixes and the exit tests), scan_b the
+// wave-uniform tail (first exit, ties, the new sum).
+struct ScanStep {
+  double T[kScanPer];  // A + prefix through element k of this lane
+  double A, sg;
+  int e;
+  unsigned bigm, tiem, hardm;
+};
+__device__ __forceinline__ void scan_a(double acc, const double (&x)[kScanPer], int c, int lane, ScanStep &s) {
+  s.e = __builtin_amdgcn_frexp_exp(acc);  // |acc| in [2^(e-1), 2^e)
+  s.sg = acc < 0.0 ? -1.0 : 1.0;
+  s.A = __builtin_amdgcn_ldexp(fabs(acc), 53 - s.e);
+  s.bigm = 0;
+  s.tiem = 0;
+  double run = 0.0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const double X = __builtin_amdgcn_ldexp(s.sg * x[k], 53 - s.e);
+    const double fl = floor(X);
+    const bool big = !(fabs(X) < 0x1p51);
+    const bool tie = !big && (X - fl) == 0.5;
+    s.bigm |= (big ? 1u : 0u) << k;
+    s.tiem |= (tie ? 1u : 0u) << k;
+    // a tie counts its lower neighbour; the parity pass adds 1 where it rounds up
+    run = run + (big ? 0.0 : (tie ? fl : rint(X)));
+    s.T[k] = run;
+  }
+  const double E = wave_exclusive_scan(run);
+  const int kl = min(max(c - kScanPer * lane, 0), kScanPer);  // this lane's elements
+  s.hardm = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    s.T[k] = s.A + (E + s.T[k]);
+    const bool hard =
+        k < kl && (((s.bigm >> k) & 1u) || !(s.T[k] >= 0x1p52 + kScanMargin && s.T[k] <= 0x1p53 - kScanMargin));
+    s.hardm |= (hard ? 1u : 0u) << k;
+  }
+}
+// The step's result: the new sum, the elements consumed (adv) and the length
+// of a one-by-one run to follow (seq).
+__device__ __forceinline__ double scan_b(ScanStep &s, const double (&x)[kScanPer], int c, int lane, int &adv, int &seq) {
+  const int pos0 = kScanPer * lane;  // this lane's positions in the step
+  int fh = c;  // the first element that must be added for real
+  {
+    const uint64_t hb = __ballot(s.hardm != 0);
+    if (hb) {
+      const int lf = __builtin_ctzll(hb);
+      fh = kScanPer * lf + __builtin_amdgcn_readlane(__builtin_ctz(s.hardm | (1u << kScanPer)), lf);
+    }
+  }
+  // ties before fh, in order: round half to even on the corrected prefix
+  {
+    unsigned tm = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k)
+      if (pos0 + k < fh) tm |= s.tiem & (1u << k);
+    int nt = 0;
+    for (uint64_t tb = __ballot(tm != 0); tb; tb = __ballot(tm != 0)) {  // wave-uniform
+      const int lt = __builtin_ctzll(tb);
+      const int kt = __builtin_ctz((unsigned)__builtin_amdgcn_readlane((int)tm, lt));
+      const int q = kScanPer * lt + kt;
+      if (nt == kScanMaxTies) {  // too many ties for the margin: this one is added for real
+        fh = q;
+        break;
+      }
+      ++nt;
+      // (every selection below reads the arrays at static indices: a
+      // selection by a run-time index is lowered to a scratch array)
+      double Tq = 0.0;
+#pragma unroll
+      for (int k = 0; k < kScanPer; ++k) {
+        const double tk = lane_d(s.T[k], lt);
+        Tq = kt == k ? tk : Tq;
+      }
+      if ((long long)Tq & 1) {  // odd: the tie rounds up, and so does every later prefix
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k)
+          if (pos0 + k >= q) s.T[k] += 1.0;
+      }
+      if (lane == lt) tm &= ~(1u << kt);
+    }
+  }
+  if (fh == c) {
+    // the last element's prefix: that lane's last prefix (positions past c
+    // hold zeros, which move no prefix, and every tie correction moves them all)
+    adv = c;
+    return s.sg * __builtin_amdgcn_ldexp(lane_d(s.T[kScanPer - 1], (c - 1) / kScanPer), s.e - 53);
+  }
+  const int lf = fh / kScanPer, fk = fh % kScanPer;
+  double Tpre = 0.0, xf = 0.0;  // lane lf's prefix before position fk and its element fk
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const double xk = lane_d(x[k], lf), tk = lane_d(s.T[k], lf);
+    xf = fk == k ? xk : xf;
+    Tpre = fk - 1 == k ? tk : Tpre;
+  }
+  // the prefix before fh: the previous element's (in this lane or the lane below), or A
+  double Tp = fk > 0 ? Tpre : s.A;
+  if (fk == 0 && lf > 0) Tp = lane_d(s.T[kScanPer - 1], lf - 1);
+  double acc = s.sg * __builtin_amdgcn_ldexp(Tp, s.e - 53);
+  acc = acc + xf;  // the exiting / large element, rounded for real
+  adv = fh + 1;
+  if (fh < 16) seq = 32;  // exits close together: a short one-by-one run
+  return acc;
+}
+// one by one, lane-major element order: a run after an early exit (seq), or
+// the first element onto a zero / non-finite sum
+__device__ __forceinline__ double seq_run(double acc, const double (&x)[kScanPer], int c, int &adv, int &seq) {
+  const int mm = seq > 0 ? min(seq, c) : 1;
+  for (int l = 0; l * kScanPer < mm; ++l) {
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k)
+      if (l * kScanPer + k < mm) acc = acc + lane_d(x[k], l);
+  }
+  seq = seq > 0 ? seq - mm : 0;
+  adv = mm;
+  return acc;
+}
+__device__ __forceinline__ bool scan_ok(double acc, int seq) { return seq == 0 && acc != 0.0 && isfinite(acc); }
+
+__device__ __forceinline__ double ordered_sum_wave(double acc, const double *yv, const unsigned short *m, int n, int S,
+                                                   int lane, int &steps) {
   int i = 0, seq = 0;
   while (i < n) {  // wave-uniform
     ++steps;
@@ -492,111 +617,50 @@ __device__ double ordered_sum_wave(double acc, const double *yv, const unsigned 
       const int j = i + kScanPer * lane + k;
       x[k] = j < n ? yv[2 * min((int)m[j], S - 1)] : 0.0;
     }
-    if (seq > 0 || !(acc != 0.0 && isfinite(acc))) {  // one by one, lane-major element order
-      const int mm = seq > 0 ? min(seq, c) : 1;
-      for (int l = 0; l * kScanPer < mm; ++l) {
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k)
-          if (l * kScanPer + k < mm) acc = acc + lane_d(x[k], l);
-      }
-      seq = seq > 0 ? seq - mm : 0;
-      i += mm;
-      continue;
-    }
-    const int e = __builtin_amdgcn_frexp_exp(acc);  // |acc| in [2^(e-1), 2^e)
-    const double sg = acc < 0.0 ? -1.0 : 1.0;
-    const double A = __builtin_amdgcn_ldexp(fabs(acc), 53 - e);
-    double T[kScanPer];
-    unsigned bigm = 0, tiem = 0;
-    double run = 0.0;
-#pragma unroll
-    for (int k = 0; k < kScanPer; ++k) {
-      const double X = __builtin_amdgcn_ldexp(sg * x[k], 53 - e);
-      const double fl = floor(X);
-      const bool big = !(fabs(X) < 0x1p51);
-      const bool tie = !big && (X - fl) == 0.5;
-      bigm |= (big ? 1u : 0u) << k;
-      tiem |= (tie ? 1u : 0u) << k;
-      // a tie counts its lower neighbour; the parity pass below adds 1 where it rounds up
-      run = run + (big ? 0.0 : (tie ? fl : rint(X)));
-      T[k] = run;
-    }
-    const double E = wave_exclusive_scan(run);
-    const int kl = min(max(c - kScanPer * lane, 0), kScanPer);  // this lane's elements
-    const int pos0 = kScanPer * lane;                           // their positions in the step
-    unsigned hardm = 0;
-#pragma unroll
-    for (int k = 0; k < kScanPer; ++k) {
-      T[k] = A + (E + T[k]);
-      const bool hard = k < kl && (((bigm >> k) & 1u) || !(T[k] >= 0x1p52 + kScanMargin && T[k] <= 0x1p53 - kScanMargin));
-      hardm |= (hard ? 1u : 0u) << k;
-    }
-    int fh = c;  // the first element that must be added for real
-    {
-      const uint64_t hb = __ballot(hardm != 0);
-      if (hb) {
-        const int lf = __builtin_ctzll(hb);
-        fh = kScanPer * lf + __builtin_amdgcn_readlane(__builtin_ctz(hardm | (1u << kScanPer)), lf);
-      }
-    }
-    // ties before fh, in order: round half to even on the corrected prefix
-    {
-      unsigned tm = 0;
-#pragma unroll
-      for (int k = 0; k < kScanPer; ++k)
-        if (pos0 + k < fh) tm |= tiem & (1u << k);
-      int nt = 0;
-      for (uint64_t tb = __ballot(tm != 0); tb; tb = __ballot(tm != 0)) {  // wave-uniform
-        const int lt = __builtin_ctzll(tb);
-        const int kt = __builtin_ctz((unsigned)__builtin_amdgcn_readlane((int)tm, lt));
-        const int q = kScanPer * lt + kt;
-        if (nt == kScanMaxTies) {  // too many ties for the margin: this one is added for real
-          fh = q;
-          break;
-        }
-        ++nt;
-        double ts = T[0];
-#pragma unroll
-        for (int k = 1; k < kScanPer; ++k)
-          if (kt == k) ts = T[k];
-        const double Tq = lane_d(ts, lt);
-        if ((long long)Tq & 1) {  // odd: the tie rounds up, and so does every later prefix
-#pragma unroll
-          for (int k = 0; k < kScanPer; ++k)
-            if (pos0 + k >= q) T[k] += 1.0;
-        }
-        if (lane == lt) tm &= ~(1u << kt);
-      }
-    }
-    if (fh == c) {
-      const int kk = (c - 1) % kScanPer;
-      double Tl = T[0];
-#pragma unroll
-      for (int k = 1; k < kScanPer; ++k)
-        if (kk == k) Tl = T[k];
-      acc = sg * __builtin_amdgcn_ldexp(lane_d(Tl, (c - 1) / kScanPer), e - 53);
-      i += c;
+    int adv;
+    if (!scan_ok(acc, seq)) {
+      acc = seq_run(acc, x, c, adv, seq);
     } else {
-      const int lf = fh / kScanPer, fk = fh % kScanPer;
-      double Tpre = T[0], xf = x[0];
-#pragma unroll
-      for (int k = 1; k < kScanPer; ++k) {
-        if (fk == k) xf = x[k];
-        if (fk - 1 == k) Tpre = T[k];
-      }
-      // the prefix before fh: the previous element's (in this lane or the lane below), or A
-      double Tp = fk > 0 ? lane_d(Tpre, lf) : A;
-      if (fk == 0 && lf > 0) {
-        double Tlast = T[kScanPer - 1];
-        Tp = lane_d(Tlast, lf - 1);
-      }
-      acc = sg * __builtin_amdgcn_ldexp(Tp, e - 53);
-      acc = acc + lane_d(xf, lf);  // the exiting / large element, rounded for real
-      i += fh + 1;
-      if (fh < 16) seq = 32;  // exits close together: a short one-by-one run
+      ScanStep st;
+      scan_a(acc, x, c, lane, st);
+      acc = scan_b(st, x, c, lane, adv, seq);
     }
+    i += adv;
   }
   return acc;
+}
+
+// Both chains over the one-wave kernel's LDS value list (the members' symbols
+// in order): the same steps as ordered_sum_wave2, values read straight from
+// the list (positions past n read the list's last member and count 0).
+__device__ __forceinline__ void ordered_sum_vals2(double &acc0, double &acc1, const double2 *vals, int n, int lane,
+                                                  int &steps) {
+  int i0 = 0, i1 = 0, seq0 = 0, seq1 = 0;
+  while (i0 < n || i1 < n) {  // wave-uniform
+    ++steps;
+    const int c0 = max(min(64 * kScanPer, n - i0), 0), c1 = max(min(64 * kScanPer, n - i1), 0);
+    double x0[kScanPer], x1[kScanPer];
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      const int j0 = i0 + kScanPer * lane + k, j1 = i1 + kScanPer * lane + k;
+      const double v0 = vals[min(j0, n - 1)].x, v1 = vals[min(j1, n - 1)].y;
+      x0[k] = j0 < n ? v0 : 0.0;
+      x1[k] = j1 < n ? v1 : 0.0;
+    }
+    ScanStep s0, s1;  // both computed (a finished chain's is ignored)
+    scan_a(acc0, x0, c0, lane, s0);
+    scan_a(acc1, x1, c1, lane, s1);
+    if (c0 > 0) {
+      int adv;
+      acc0 = scan_ok(acc0, seq0) ? scan_b(s0, x0, c0, lane, adv, seq0) : seq_run(acc0, x0, c0, adv, seq0);
+      i0 += adv;
+    }
+    if (c1 > 0) {
+      int adv;
+      acc1 = scan_ok(acc1, seq1) ? scan_b(s1, x1, c1, lane, adv, seq1) : seq_run(acc1, x1, c1, adv, seq1);
+      i1 += adv;
+    }
+  }
 }
 
 // Lower bound of |sqrt(hi) - sqrt(lo)| (true distances of the fp cluster
@@ -658,6 +722,45 @@ __device__ __forceinline__ bool member0_margin(const double2 *cl, double yr, dou
     }
   }
   return member0_slow<KC>(cl, yr, yi);
+}
+
+// member0_margin's fast path without branches (the one-wave kernel): returns
+// whether the screen decided; then m is the decision and g its margin, else
+// the caller runs member0_slow (g = 0).  The range test d2_ok of every
+// distance is taken on the high dwords as unsigned integers (NaN and inf
+// included): hi(d) > hi(1e-290) and hi(d) < hi(1e290) imply 1e-290 < d <
+// 1e290, so the screen decides only where member0_margin does, with the same
+// operations on the same values (elsewhere the exact decision, with g = 0).
+constexpr unsigned kD2HiLo = 0x03b8f2b0u;  // high dword of 1e-290
+constexpr unsigned kD2HiHi = 0x7c2485ceu;  // high dword of 1e290
+template <int KC>
+__device__ __forceinline__ bool screen0(const double2 *cl, double yr, double yi, bool &m, double &g) {
+  double d0 = 0.0, m1 = 0.0;
+  unsigned hmin = 0xffffffffu, hmax = 0u;
+#pragma unroll 8
+  for (int k = 0; k < KC; ++k) {
+    const double2 c = cl[k];
+    const double dr = c.x - yr, di = c.y - yi;
+    const double d = dr * dr + di * di;
+    const unsigned h = (unsigned)__double2hiint(d);
+    hmin = min(hmin, h);
+    hmax = max(hmax, h);
+    if (k == 0)
+      d0 = d;
+    else if (k == 1)
+      m1 = d;
+    else
+      m1 = fmin(m1, d);  // no NaN reaches a decided screen
+  }
+  const bool in = d0 < m1 * (1.0 - kTieBand);
+  const bool out = d0 > m1 * (1.0 + kTieBand);
+  const double lo = in ? d0 : m1, hi = in ? m1 : d0;
+  // dist_margin(lo, hi), branch-free
+  const double num = (hi - lo) - 1e-13 * (hi + lo);
+  const double q = num * (double)__builtin_amdgcn_rsqf((float)hi) * (0.5 * (1.0 - 1e-5)) - 1e-13 * (hi + 1.0);
+  g = (lo >= 1e-30 && hi <= 1e30 && q > 0.0) ? q : 0.0;
+  m = in;
+  return hmin > kD2HiLo && hmax < kD2HiHi && (in || out);
 }
 
 __device__ KM_SLOW cplx cdiv_slow(cplx n, cplx dd) { return kml_cdiv(n, dd); }
@@ -1019,6 +1122,281 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
   }
 }
 
+// ---------------------------------------------------------------------------
+// One wave per codeword (the production k-means).  The fused kernel above is
+// capped at 8 codewords per CU by its LDS copy of the symbols (16 S bytes) and
+// by its two 116-register waves, and each codeword is a chain of dependent
+// steps: the kernel runs at the latency of that chain times the number of
+// codeword rounds (19.9 iterations x ~26 K cycles, 18 % VALU busy).  Here a
+// codeword is one wave with no LDS copy of y: the symbols are read where they
+// lie (HBM, then L2 / Infinity Cache for the iterations' re-reads: coalesced
+// 64-symbol words for the assignment, a gather of the listed members for the
+// sums); a word's membership bits and drift threshold live in the registers of
+// lane = word (S <= 4096); LDS holds only the member index list and the
+// cluster points, ~1.3 KB per codeword.  Residency is then set by registers
+// (<= 128: 16 codewords per CU) and there is no workgroup barrier at all.
+// The steps are those of km_fused_kernel (same screens, margins, drift bound,
+// binade scans and divisions): the real and the imaginary chains are summed
+// by the same wave one after the other.
+#ifndef KML_KM_WAVE_OCC
+#define KML_KM_WAVE_OCC 4  // waves per SIMD (registers <= 512 / OCC)
+#endif
+constexpr int kWaveWpg = 4;  // codewords (waves) per workgroup: independent, no barrier between them
+struct KmWaveLds {
+  int cap, off_cl, stride;
+};
+__host__ __device__ constexpr KmWaveLds km_wave_lds(int S, int KC) {
+  const int cap = ((S + 1) / 2 + 7) & ~7;  // cluster 0 of a constellation of >= 2 points
+  const int off_cl = 16 * cap;
+  return KmWaveLds{cap, off_cl, off_cl + 16 * KC};
+}
+
+template <int KC>
+__global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(KML_KM_WAVE_OCC))) void km_wave_kernel(
+    const double *__restrict__ cons, const double *__restrict__ rot, const double2 *__restrict__ y, int S, int iters,
+    int B, double2 *__restrict__ h_hat, double2 *__restrict__ h4, double2 *__restrict__ hat_out, int incremental,
+    int scan) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char kmem[];
+  const KmWaveLds L = km_wave_lds(S, KC);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cw = blockIdx.x * kWaveWpg + wave;
+  if (cw >= B) return;  // wave-uniform; the waves of a workgroup never wait for each other
+  double2 *vals = reinterpret_cast<double2 *>(kmem + wave * L.stride);           // [cap] the members' symbols, in order
+  double2 *cl = reinterpret_cast<double2 *>(kmem + wave * L.stride + L.off_cl);  // [KC] cluster points
+  const int Sw = (S + 63) / 64;
+#if KML_STAMPS
+  unsigned long long km_prev = __builtin_amdgcn_s_memtime();
+  unsigned long long km_acc[KS_STEPS + 1] = {};
+  KM_COUNT(KS_CW, 1);
+#endif
+  const double2 *yy = y + (long long)cw * S;
+
+  // ---- first max |y| (kmeans.cc:17-22), screened like first_max_abs: one
+  // pass keeps each lane's largest squared norm (first index) and its second
+  // largest; when no lane holds two symbols inside the tie band of the
+  // maximum, the band's candidates are the lanes' maxima and one exact hypot
+  // each decides (else the band is rescanned)
+  int mi;
+  {
+    double d1 = -1.0, d2 = -1.0;
+    int j1 = 0;
+    bool ex = false;
+#pragma unroll 6
+    for (int j = lane; j < S; j += 64) {
+      const double2 v = yy[j];
+      const double d = v.x * v.x + v.y * v.y;
+      if (!d2_ok(d) && !(d == 0.0)) ex = true;
+      if (d > d1) {
+        d2 = d1;
+        d1 = d;
+        j1 = j;
+      } else if (d > d2) {
+        d2 = d;
+      }
+    }
+    const double best = wave_max(d1);
+    const double band = best * (1.0 - kTieBand);
+    if (__ballot(ex) == 0 && best > 0.0 && __ballot(d2 >= band) == 0) {
+      const bool cand = d1 >= band;
+      const double h = cand ? kml_hypot(yy[j1].x, yy[j1].y) : -1.0;
+      const double hb = wave_max(h);
+      mi = wave_min_i(cand && h == hb ? j1 : 0x7fffffff);
+    } else if (__ballot(ex) == 0 && best > 0.0) {
+      double hb = -1.0;  // max exact |y| among the band's candidates
+      for (int j = lane; j < S; j += 64) {
+        const double2 v = yy[j];
+        if (v.x * v.x + v.y * v.y >= band) hb = fmax(hb, kml_hypot(v.x, v.y));
+      }
+      hb = wave_max(hb);
+      int jm = 0x7fffffff;  // the first index attaining it
+      for (int j = lane; j < S; j += 64) {
+        const double2 v = yy[j];
+        if (v.x * v.x + v.y * v.y >= band && kml_hypot(v.x, v.y) == hb) jm = min(jm, j);
+      }
+      mi = wave_min_i(jm);
+    } else {  // the reference loop, sequentially (non-finite / extreme / all-zero input)
+      int m = 0;
+      if (lane == 0) {
+        double h0 = kml_hypot(yy[0].x, yy[0].y);
+        for (int j = 1; j < S; ++j) {
+          const double h = kml_hypot(yy[j].x, yy[j].y);
+          if (h0 < h) {
+            h0 = h;
+            m = j;
+          }
+        }
+      }
+      mi = __builtin_amdgcn_readlane(m, 0);
+    }
+  }
+  const cplx c0{cons[0], cons[1]};
+  const CdivConst c0k = cdiv_prepare(c0);
+  cplx hat = kml_cdiv(cplx{yy[mi].x, yy[mi].y}, c0);  // kmeans.cc:25
+  // 1 / (2 Cmax), rounded down (|c| <= |re| + |im|)
+  double cb = 0.0;
+  for (int k = 0; k < KC; ++k) cb = fmax(cb, fabs(cons[2 * k]) + fabs(cons[2 * k + 1]));
+  const double inv2c = cb > 0.0 ? (0.5 / cb) * (1.0 - 1e-12) : 0.0;
+  cplx prevk{0.0, 0.0};  // lane k < KC: cluster k of the previous iteration (tempClusters, zero at first)
+  const cplx ck = lane < KC ? cplx{cons[2 * lane], cons[2 * lane + 1]} : cplx{0.0, 0.0};  // lane k < KC: c[k]
+  cplx hprev = hat;
+  double drift = 0.0;  // D, the same value in every lane
+  double sr = 0.0, si = 0.0;  // cumulative cluster-0 sum (kmeans.cc:33-34, 46)
+  int cnt = 0, nmem = 0;
+  // lane w < Sw: word w's membership bits and its threshold min(D(ref) + g / (2 Cmax)); -1: assign
+  uint64_t wb = 0;
+  float wt = -1.0f;
+  const double *yv = reinterpret_cast<const double *>(yy);
+  KM_STAMP(KS_PRO);
+  for (int it = 0; it < iters; ++it) {
+    // clusters_[k] = c[k] * hatH and the convergence test against tempClusters
+    // (kmeans.cc:26-28 / 72-74, 47-56), lanes k < KC
+    {
+      bool same = true;
+      if (lane < KC) {
+        const cplx p = kml_cmul(ck, hat);
+        cl[lane] = make_double2(p.re, p.im);
+        same = (p.re == prevk.re) && (p.im == prevk.im);
+        prevk = p;
+      }
+      const bool conv = __ballot(!same) == 0;
+      __builtin_amdgcn_wave_barrier();  // the cluster stores precede the loads below (LDS in order per wave)
+      KM_STAMP(KS_CLUSTERS);
+      if (conv) break;  // the reference breaks after an assignment it then discards
+    }
+    KM_COUNT(KS_ITERS, 1);
+    {
+      const double dd = (fabs(hat.re - hprev.re) + fabs(hat.im - hprev.im)) * (1.0 + 1e-15) +
+                        0x1p-48 * (fabs(hat.re) + fabs(hat.im) + fabs(hprev.re) + fabs(hprev.im));
+      drift = (drift + dd) * (1.0 + 0x1p-50);
+      hprev = hat;
+    }
+    // assignment (kmeans.cc:36-46) of the words whose decisions the drift may
+    // have changed; two words per pass (independent loads, screens and minima)
+    int chg = 0;
+    {
+      uint64_t need = __ballot(lane < Sw && (!incremental || !(drift < (double)wt)));
+      while (need) {  // wave-uniform: up to 4 flagged words per pass, their symbols loaded together
+        constexpr int NG = KML_KM_GROUP;
+        int qs[NG];
+#pragma unroll
+        for (int u = 0; u < NG; ++u) {
+          qs[u] = need ? __builtin_ctzll(need) : -1;
+          need &= need - 1;
+        }
+        double2 v[NG];
+#pragma unroll
+        for (int u = 0; u < NG; ++u) v[u] = yy[min((qs[u] < 0 ? qs[0] : qs[u]) * 64 + lane, S - 1)];
+#pragma unroll
+        for (int u = 0; u < NG; ++u) {
+          if (qs[u] < 0) break;
+          const bool valid = qs[u] * 64 + lane < S;
+          bool m;
+          double g;
+          const bool dec = screen0<KC>(cl, v[u].x, v[u].y, m, g);
+          if (__ballot(valid && !dec))
+            if (valid && !dec) {  // tie band / range: the exact decision
+              m = member0_slow<KC>(cl, v[u].x, v[u].y);
+              g = 0.0;
+            }
+          // D + g / (2 Cmax), rounded down; past the float range a finite 2^127
+          const double td = (drift + g * inv2c) * (1.0 - 0x1p-20);
+          const float t = wave_min_f(valid ? (td < 0x1p127 ? (float)td : 0x1p127f) : INFINITY);
+          const uint64_t bits = __ballot(valid && m);
+          if (it == 0 || bits != lane_u64(wb, qs[u])) chg = 1;
+          if (lane == qs[u]) {
+            wb = bits;
+            wt = t;
+          }
+        }
+        KM_COUNT(KS_WORDS, 1);
+      }
+    }
+    KM_STAMP(KS_ASSIGN);
+    if (chg) {  // members changed: rebuild the value list (word by word, coalesced loads, lanes = symbols)
+      KM_COUNT(KS_COMPACTIONS, 1);
+      const int c = __popcll(wb);
+      const int incl = wave_inclusive_scan_i(c);
+      const int excl = incl - c;
+      nmem = __builtin_amdgcn_readlane(incl, 63);
+      for (int w0 = 0; w0 < Sw; w0 += 6) {  // six words' loads in flight
+        double2 v[6];
+#pragma unroll
+        for (int u = 0; u < 6; ++u) v[u] = yy[min((w0 + u) * 64 + lane, S - 1)];  // past the last word: a repeat
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+          if (w0 + u < Sw) {
+            const uint64_t bits = lane_u64(wb, w0 + u);
+            const int p = __builtin_amdgcn_readlane(excl, w0 + u) + __popcll(bits & ((1ull << lane) - 1));
+            if (((bits >> lane) & 1) && p < L.cap) vals[p] = v[u];
+          }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    KM_STAMP(KS_COMPACT);
+    const int n = nmem;
+    cnt += n;
+    const DdRcp yc = dd_rcp((double)cnt);  // the update's divisor, ahead of the sums
+    if (n > L.cap) {  // more members than the list holds (degenerate input): straight from the words
+      double acc = lane == 0 ? sr : si;  // lane 0: real chain, lane 1: imaginary chain, ascending j
+      for (int w = 0; w < Sw; ++w) {
+        const uint64_t bits = lane_u64(wb, w);
+        if (lane < 2)
+          for (uint64_t b = bits; b; b &= b - 1) acc = acc + yv[2 * (w * 64 + __builtin_ctzll(b)) + lane];
+      }
+      sr = lane_d(acc, 0);
+      si = lane_d(acc, 1);
+    } else if (scan) {
+      int steps = 0;
+      ordered_sum_vals2(sr, si, vals, n, lane, steps);
+      KM_COUNT(KS_STEPS, steps);
+    } else {  // lane 0: real chain, lane 1: imaginary chain
+      double acc = lane == 0 ? sr : si;
+      if (lane < 2)
+        for (int i = 0; i < n; ++i) acc = acc + reinterpret_cast<const double *>(vals)[2 * i + lane];
+      sr = lane_d(acc, 0);
+      si = lane_d(acc, 1);
+    }
+    KM_STAMP(KS_SUM);
+    {
+      const cplx m0 = cdiv_count(sr, si, cnt, yc);  // kmeans.cc:59-62
+      hat = cdiv_const(m0, c0, c0k);                // kmeans.cc:64-71
+    }
+    KM_STAMP(KS_UPDATE);
+  }
+#if KML_STAMPS
+  if (tid == 0)
+    for (int i = 0; i <= KS_STEPS; ++i) atomicAdd(&kml_km_stamps[i], km_acc[i]);
+#endif
+  if (lane == 0) {
+    if (hat_out) hat_out[cw] = make_double2(hat.re, hat.im);  // the final hatH (clusters_ = c[k] * hatH)
+    const cplx hh = kml_cdiv(kml_cmul(c0, hat), c0);  // simulator.cc:145
+    h_hat[cw] = make_double2(hh.re, hh.im);
+    for (int j = 0; j < 4; ++j) {  // simulator.cc:146-148
+      const cplx r = kml_cmul(hh, cplx{rot[2 * j], rot[2 * j + 1]});
+      h4[(long long)cw * 4 + j] = make_double2(r.re, r.im);
+    }
+  }
+}
+
+template <int KC>
+bool run_kmeans_wave(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
+                     double2 *h_hat, double2 *h4, double2 *hat_out, hipStream_t s, hipError_t &err) {
+  const size_t lds = (size_t)kWaveWpg * km_wave_lds(S, KC).stride;
+  if (S > 64 * kFusedMaxW || lds > 160 * 1024) return false;
+  const char *e = getenv("KML_KMEANS");
+  if (!e || e[0] != 'w') return false;  // KML_KMEANS=wave (A/B; the default is km_fused_kernel)
+  err = hipFuncSetAttribute((const void *)km_wave_kernel<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return true;
+  int incremental = 1, scan = 1;
+  if (const char *e = getenv("KML_KM_INCR")) incremental = e[0] != '0';
+  if (const char *e = getenv("KML_KM_SCAN")) scan = e[0] != '0';
+  hipLaunchKernelGGL(km_wave_kernel<KC>, dim3((B + kWaveWpg - 1) / kWaveWpg), dim3(64 * kWaveWpg), lds, s, cons, rot,
+                     y, S, iters, B, h_hat, h4, hat_out, incremental, scan);
+  err = hipGetLastError();
+  return true;
+}
+
 template <int KC>
 bool run_kmeans_fused(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
                       double2 *h_hat, double2 *h4, double2 *hat_out, hipStream_t s, hipError_t &err) {
@@ -1044,6 +1422,7 @@ template <int KC>
 hipError_t run_kmeans(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
                       KmState *st, uint64_t *mem, double2 *h_hat, double2 *h4, double2 *hat_out, hipStream_t s) {
   hipError_t ferr = hipSuccess;
+  if (run_kmeans_wave<KC>(cons, rot, y, S, iters, B, h_hat, h4, hat_out, s, ferr)) return ferr;
   if (run_kmeans_fused<KC>(cons, rot, y, S, iters, B, h_hat, h4, hat_out, s, ferr)) return ferr;
   const int Sw = (S + 63) / 64;
   const dim3 lanes((B + 63) / 64), l64(64);

@@ -481,10 +481,11 @@ static bool plan_partition_uncached(const LdpcCode &L, int G, PartitionPlan &out
   // phase's bank conflicts (write bins of the slot, read bins of the c2v half:
   // bp_coop.hip part_c2v_half — bit 2 of the row for row slots, of the slot
   // index for mirror slots)
-  // each member's INTERIOR columns (every edge's row its own) last: the
-  // partitioned kernel runs them before the cut-edge c2v receive, the
-  // boundary columns after it (bp_coop.hip, KML_PART_SPLIT); the annealing
-  // below keeps the two runs apart
+  // each member's INTERIOR columns (every edge's row its own) last, so the
+  // boundary columns, whose v2c the partners wait for, are stored first; the
+  // annealing below keeps the two runs apart (a VN phase split around the c2v
+  // receive, interior columns first, measured slower: 8.75 vs 8.20 ms per 4096
+  // PEG8064 codewords, profiles/r05_ab2_summary.txt)
   std::vector<int> nbound(G, NG);
   for (int g = 0; g < G; g++) {
     auto interior = [&](int j) {

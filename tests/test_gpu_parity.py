@@ -409,7 +409,9 @@ def test_fused_demap_matches_separate(data_dir, blind, monkeypatch):
     ("PEG2304regular0.5.txt", "4bit_16QAM_phi1.txt", 8.0, 50),
     ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", 6.77, 30),
 ])
-def test_kmeans_vs_oracle(data_dir, matrix, modem, snr, n):
+@pytest.mark.parametrize("kernel", ["fused", "wave"])
+def test_kmeans_vs_oracle(data_dir, matrix, modem, snr, n, kernel, monkeypatch):
+    monkeypatch.setenv("KML_KMEANS", kernel)
     ctx = ctx_for(data_dir, matrix, modem, False)
     oc = oracle_for(data_dir, matrix, False)
     om = O.Modem(os.path.join(data_dir, modem))
@@ -453,7 +455,7 @@ def test_kmeans_adversarial_ties(data_dir, modem):
         assert np.array_equal(hh[b], ref, equal_nan=True), b
 
 
-@pytest.mark.parametrize("mode", ["default", "sequential_sum", "owned_words"])
+@pytest.mark.parametrize("mode", ["default", "sequential_sum", "owned_words", "wave", "wave_sequential_sum"])
 @pytest.mark.parametrize("modem", ["2bits_QPSK.txt", "4bit_16QAM_Gray.txt", "6bits_64QAM_Gray.txt"])
 def test_kmeans_cumulative_sum_adversarial(data_dir, modem, mode, monkeypatch):
     """The fused k-means' cumulative cluster-0 sums (kmeans.hip
@@ -463,10 +465,14 @@ def test_kmeans_cumulative_sum_adversarial(data_dir, modem, mode, monkeypatch):
     coarse dyadic grid (ties), a cluster-0 centre on an axis (sums that change
     sign), tiny and huge channels (extreme binades; thresholds past the float
     range), NaN / inf symbols (the complex products' infinity recovery) and
-    realistic frames; with the default kernel, the two-lane sequential sums
-    (KML_KM_SCAN=0) and each wave assigning its own words (KML_KM_BAL=0)."""
-    monkeypatch.setenv("KML_KM_SCAN", "0" if mode == "sequential_sum" else "1")
+    realistic frames; with the default kernel (two waves per codeword), its
+    two-lane sequential sums (KML_KM_SCAN=0) and each wave assigning its own
+    words (KML_KM_BAL=0), and the one-wave kernel (KML_KMEANS=wave: value
+    list in LDS, both chains per scan step) with and without its scans."""
+    monkeypatch.setenv("KML_KM_SCAN", "0" if mode.endswith("sequential_sum") else "1")
     monkeypatch.setenv("KML_KM_BAL", "0" if mode == "owned_words" else "1")
+    if mode.startswith("wave"):
+        monkeypatch.setenv("KML_KMEANS", "wave")
     matrix = "PEG8064regular0.5.txt" if "64QAM" in modem else "PEG2304regular0.5.txt"
     ctx = ctx_for(data_dir, matrix, modem, False)
     om = O.Modem(os.path.join(data_dir, modem))
