@@ -120,6 +120,16 @@ __device__ __forceinline__ unsigned ld_rlx(const unsigned *p) {  // L1-bypassing
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Abort the cooperative launch: abort[0] = 1 stops every poll; the first
+// aborter also records where it gave up in abort[1] (site << 24 | workgroup):
+// 1 group barrier, 2 v2c mailbox poll, 3 c2v mailbox poll, 4 early-stop flag
+// poll (bp_coop_aborted reports it).
+enum { kAbortBarrier = 1, kAbortV2c = 2, kAbortC2v = 3, kAbortFlag = 4 };
+__device__ __forceinline__ void coop_abort(unsigned *abort, unsigned site) {
+  atomicCAS(abort + 1, 0u, (site << 24) | (blockIdx.x & 0xFFFFFFu));
+  __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // loads of data other members wrote: bypass the vector L1
 template <class T>
 __device__ __forceinline__ T ld_nt(const T *p) {
@@ -197,7 +207,7 @@ __device__ __forceinline__ int part_barrier(GroupSync *gs, unsigned long long *s
       v = ld_rlx64(&gs->bar2[p]);
       if ((unsigned)v >= (unsigned)st[p]) break;
       if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
-        __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        coop_abort(abort, kAbortBarrier);
         r = -1;
         break;
       }
@@ -598,7 +608,7 @@ __device__ __forceinline__ bool poll_entries(const int (&ent)[R], __amdgpu_buffe
       }
     if (!pend) return true;
     if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
-      __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      coop_abort(abort, W == 2 ? kAbortV2c : kAbortC2v);
       return false;
     }
     if (KML_POLL_SLEEP) __builtin_amdgcn_s_sleep(1);
@@ -728,7 +738,7 @@ __device__ __forceinline__ int part_iterations_tagged(
           v = spin == 0 ? vflag : ld_rlx64(&gs->mflag[(g - 1) & 1][tid]);  // first: the load issued before VN
           if ((v >> 2) == (unsigned long long)g) break;
           if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
-            __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            coop_abort(abort, kAbortFlag);
             *sdead = 1;
             break;
           }
@@ -1205,7 +1215,7 @@ hipError_t launch_part_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int
   e = hipMemsetAsync(a.queue, 0, sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
   // the group blocks, and the abort word unless this launch follows one whose abort must persist
-  e = hipMemsetAsync(a.gsync, 0, sizeof(GroupSync) * (size_t)groups + (reset_abort ? sizeof(unsigned) : 0), s);
+  e = hipMemsetAsync(a.gsync, 0, sizeof(GroupSync) * (size_t)groups + (reset_abort ? 2 * sizeof(unsigned) : 0), s);
   if (e != hipSuccess) return e;
   if (TAGGED) {  // every tagged mailbox word starts with tag 1 (the first iteration writes tag 0)
     e = hipMemsetAsync(a.gslots, 0xFF, sizeof(double2) * (size_t)groups * c.E, s);
@@ -1347,12 +1357,14 @@ hipError_t bp_coop_raise_abort(const BpLaunch &a, int groups, hipStream_t s) {
   return hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(reinterpret_cast<GroupSync *>(a.gsync) + groups), 1u, 1, s);
 }
 
-// Did the last cooperative launch abort (a group barrier timed out)?
-bool bp_coop_aborted(const BpLaunch &a, int groups, hipStream_t s) {
-  unsigned v = 0;
-  hipMemcpyAsync(&v, reinterpret_cast<GroupSync *>(a.gsync) + groups, sizeof(v), hipMemcpyDeviceToHost, s);
+// Did the last cooperative launch abort (a poll timed out)?  why: the first
+// aborter's site << 24 | workgroup (0: raised by the host, kml_debug_inject_abort).
+bool bp_coop_aborted(const BpLaunch &a, int groups, hipStream_t s, unsigned *why) {
+  unsigned v[2] = {0, 0};
+  hipMemcpyAsync(v, reinterpret_cast<GroupSync *>(a.gsync) + groups, sizeof(v), hipMemcpyDeviceToHost, s);
   hipStreamSynchronize(s);
-  return v != 0;
+  if (why) *why = v[1];
+  return v[0] != 0;
 }
 
 }  // namespace kml

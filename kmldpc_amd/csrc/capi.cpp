@@ -510,8 +510,15 @@ int sync(kml_ctx *c) {
     c->coop_pending = false;
     kml::BpLaunch a;
     a.gsync = c->d_gsync.p;
-    if (kml::bp_coop_aborted(a, c->coop_groups, c->stream))
-      return fail(c, KML_E_HIP, "cooperative BP kernel aborted (a group barrier timed out)");
+    unsigned why = 0;
+    if (kml::bp_coop_aborted(a, c->coop_groups, c->stream, &why)) {
+      static const char *const site[] = {"raised by the host", "group barrier", "v2c mailbox poll", "c2v mailbox poll",
+                                         "early-stop flag poll"};
+      const unsigned k = why >> 24;
+      return fail(c, KML_E_HIP,
+                  std::string("cooperative BP kernel aborted (a group barrier timed out): ") + (k < 5 ? site[k] : "?") +
+                      (why ? ", workgroup " + std::to_string(why & 0xFFFFFFu) : std::string()));
+    }
   }
   return KML_OK;
 }

@@ -122,7 +122,7 @@ int bp_part_group_size(int N, int M, int E, int dv_max, int dc_max, int regular)
 bool part_plan_fits(int G, int N, int M, int E, int ncut, int mirror_max, int xmax);
 // Name of the cooperative kernel launch_bp_coop runs for this code.
 const char *bp_coop_family(const DevCode &c);
-bool bp_coop_aborted(const BpLaunch &a, int groups, hipStream_t s);
+bool bp_coop_aborted(const BpLaunch &a, int groups, hipStream_t s, unsigned *why = nullptr);
 // Test hook: set the abort word on the stream, as a timed-out group barrier would.
 hipError_t bp_coop_raise_abort(const BpLaunch &a, int groups, hipStream_t s);
 // Threads per workgroup of the regular kernel for this code shape, 0 if it does

@@ -451,9 +451,6 @@ __device__ __forceinline__ double ordered_sum(double acc, const double *yv, cons
 #define KML_KM_SCAN_PER 5
 #endif
 constexpr int kScanPer = KML_KM_SCAN_PER;
-#ifndef KML_KM_GROUP  // (A/B) one-wave kernel: flagged words per assignment pass
-#define KML_KM_GROUP 2
-#endif
 constexpr double kScanMargin = 64.0;      // grid steps kept from the binade ends: room for the tie corrections
 constexpr int kScanMaxTies = 32;          // ties resolved in one step (each moves later prefixes by <= 1)
 template <int CTRL, int ROWS>
@@ -630,37 +627,32 @@ __device__ __forceinline__ double ordered_sum_wave(double acc, const double *yv,
   return acc;
 }
 
-// Both chains over the one-wave kernel's LDS value list (the members' symbols
-// in order): the same steps as ordered_sum_wave2, values read straight from
-// the list (positions past n read the list's last member and count 0).
-__device__ __forceinline__ void ordered_sum_vals2(double &acc0, double &acc1, const double2 *vals, int n, int lane,
-                                                  int &steps) {
-  int i0 = 0, i1 = 0, seq0 = 0, seq1 = 0;
-  while (i0 < n || i1 < n) {  // wave-uniform
+// One chain (comp 0: real, 1: imaginary) over the LDS value list.
+__device__ __forceinline__ double ordered_sum_vals1(double acc, const double2 *vals, int comp, int n, int lane,
+                                                    int &steps) {
+  int i = 0, seq = 0;
+  const double *vv = reinterpret_cast<const double *>(vals) + comp;
+  while (i < n) {  // wave-uniform
     ++steps;
-    const int c0 = max(min(64 * kScanPer, n - i0), 0), c1 = max(min(64 * kScanPer, n - i1), 0);
-    double x0[kScanPer], x1[kScanPer];
+    const int c = min(64 * kScanPer, n - i);
+    double x[kScanPer];
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
-      const int j0 = i0 + kScanPer * lane + k, j1 = i1 + kScanPer * lane + k;
-      const double v0 = vals[min(j0, n - 1)].x, v1 = vals[min(j1, n - 1)].y;
-      x0[k] = j0 < n ? v0 : 0.0;
-      x1[k] = j1 < n ? v1 : 0.0;
+      const int j = i + kScanPer * lane + k;
+      const double v = vv[2 * min(j, n - 1)];
+      x[k] = j < n ? v : 0.0;
     }
-    ScanStep s0, s1;  // both computed (a finished chain's is ignored)
-    scan_a(acc0, x0, c0, lane, s0);
-    scan_a(acc1, x1, c1, lane, s1);
-    if (c0 > 0) {
-      int adv;
-      acc0 = scan_ok(acc0, seq0) ? scan_b(s0, x0, c0, lane, adv, seq0) : seq_run(acc0, x0, c0, adv, seq0);
-      i0 += adv;
+    int adv;
+    if (!scan_ok(acc, seq)) {
+      acc = seq_run(acc, x, c, adv, seq);
+    } else {
+      ScanStep st;
+      scan_a(acc, x, c, lane, st);
+      acc = scan_b(st, x, c, lane, adv, seq);
     }
-    if (c1 > 0) {
-      int adv;
-      acc1 = scan_ok(acc1, seq1) ? scan_b(s1, x1, c1, lane, adv, seq1) : seq_run(acc1, x1, c1, adv, seq1);
-      i1 += adv;
-    }
+    i += adv;
   }
+  return acc;
 }
 
 // Lower bound of |sqrt(hi) - sqrt(lo)| (true distances of the fp cluster
@@ -1139,17 +1131,26 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
 // binade scans and divisions): the real and the imaginary chains are summed
 // by the same wave one after the other.
 #ifndef KML_KM_WAVE_OCC
-#define KML_KM_WAVE_OCC 4  // waves per SIMD (registers <= 512 / OCC)
+#define KML_KM_WAVE_OCC 6  // waves per SIMD (registers <= 512 / OCC): 6 (80 VGPRs, 9 spilled) 2.75 ms, 5 3.04, 4 3.31
+#endif
+#ifndef KML_KM_CAPDIV
+#define KML_KM_CAPDIV 3
 #endif
 constexpr int kWaveWpg = 4;  // codewords (waves) per workgroup: independent, no barrier between them
 struct KmWaveLds {
   int cap, off_cl, stride;
 };
 __host__ __device__ constexpr KmWaveLds km_wave_lds(int S, int KC) {
-  const int cap = ((S + 1) / 2 + 7) & ~7;  // cluster 0 of a constellation of >= 2 points
+  const int cap = ((S + KML_KM_CAPDIV - 1) / KML_KM_CAPDIV + 7) & ~7;  // (A/B) larger clusters: the fallback sum
   const int off_cl = 16 * cap;
-  return KmWaveLds{cap, off_cl, off_cl + 16 * KC};
+  // then the cluster points [KC], the constellation [KC] and the launch
+  // constants (KmWaveConst): kept in LDS, not in registers across the loop
+  return KmWaveLds{cap, off_cl, off_cl + 32 * KC + 64};
 }
+struct KmWaveConst {
+  double ratio, denom, yd_hi, yd_lo, yd_k, inv2c;
+  int mode;
+};
 
 template <int KC>
 __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(KML_KM_WAVE_OCC))) void km_wave_kernel(
@@ -1164,6 +1165,8 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
   if (cw >= B) return;  // wave-uniform; the waves of a workgroup never wait for each other
   double2 *vals = reinterpret_cast<double2 *>(kmem + wave * L.stride);           // [cap] the members' symbols, in order
   double2 *cl = reinterpret_cast<double2 *>(kmem + wave * L.stride + L.off_cl);  // [KC] cluster points
+  volatile double2 *cs = cl + KC;                                                // [KC] constellation points
+  volatile KmWaveConst *kc = reinterpret_cast<volatile KmWaveConst *>(cl + 2 * KC);
   const int Sw = (S + 63) / 64;
 #if KML_STAMPS
   unsigned long long km_prev = __builtin_amdgcn_s_memtime();
@@ -1231,15 +1234,27 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
     }
   }
   const cplx c0{cons[0], cons[1]};
-  const CdivConst c0k = cdiv_prepare(c0);
   cplx hat = kml_cdiv(cplx{yy[mi].x, yy[mi].y}, c0);  // kmeans.cc:25
-  // 1 / (2 Cmax), rounded down (|c| <= |re| + |im|)
-  double cb = 0.0;
-  for (int k = 0; k < KC; ++k) cb = fmax(cb, fabs(cons[2 * k]) + fabs(cons[2 * k + 1]));
-  const double inv2c = cb > 0.0 ? (0.5 / cb) * (1.0 - 1e-12) : 0.0;
-  cplx prevk{0.0, 0.0};  // lane k < KC: cluster k of the previous iteration (tempClusters, zero at first)
-  const cplx ck = lane < KC ? cplx{cons[2 * lane], cons[2 * lane + 1]} : cplx{0.0, 0.0};  // lane k < KC: c[k]
-  cplx hprev = hat;
+  {
+    const CdivConst c0k = cdiv_prepare(c0);
+    // 1 / (2 Cmax), rounded down (|c| <= |re| + |im|)
+    double cb = 0.0;
+    for (int k = 0; k < KC; ++k) cb = fmax(cb, fabs(cons[2 * k]) + fabs(cons[2 * k + 1]));
+    if (lane == 0) {
+      kc->ratio = c0k.ratio;
+      kc->denom = c0k.denom;
+      kc->yd_hi = c0k.yd.hi;
+      kc->yd_lo = c0k.yd.lo;
+      kc->yd_k = c0k.yd.k;
+      kc->inv2c = cb > 0.0 ? (0.5 / cb) * (1.0 - 1e-12) : 0.0;
+      kc->mode = c0k.mode;
+    }
+    if (lane < KC) {
+      cs[lane].x = cons[2 * lane];
+      cs[lane].y = cons[2 * lane + 1];
+    }
+  }
+  cplx hprev = hat;  // the previous iteration's hatH (clusters_ of the previous iteration: c[k] hprev)
   double drift = 0.0;  // D, the same value in every lane
   double sr = 0.0, si = 0.0;  // cumulative cluster-0 sum (kmeans.cc:33-34, 46)
   int cnt = 0, nmem = 0;
@@ -1247,6 +1262,7 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
   uint64_t wb = 0;
   float wt = -1.0f;
   const double *yv = reinterpret_cast<const double *>(yy);
+  __builtin_amdgcn_wave_barrier();
   KM_STAMP(KS_PRO);
   for (int it = 0; it < iters; ++it) {
     // clusters_[k] = c[k] * hatH and the convergence test against tempClusters
@@ -1254,10 +1270,11 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
     {
       bool same = true;
       if (lane < KC) {
+        const cplx ck{cs[lane].x, cs[lane].y};
         const cplx p = kml_cmul(ck, hat);
+        const cplx pk = it > 0 ? kml_cmul(ck, hprev) : cplx{0.0, 0.0};  // tempClusters: the previous clusters_
         cl[lane] = make_double2(p.re, p.im);
-        same = (p.re == prevk.re) && (p.im == prevk.im);
-        prevk = p;
+        same = (p.re == pk.re) && (p.im == pk.im);
       }
       const bool conv = __ballot(!same) == 0;
       __builtin_amdgcn_wave_barrier();  // the cluster stores precede the loads below (LDS in order per wave)
@@ -1276,38 +1293,27 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
     int chg = 0;
     {
       uint64_t need = __ballot(lane < Sw && (!incremental || !(drift < (double)wt)));
-      while (need) {  // wave-uniform: up to 4 flagged words per pass, their symbols loaded together
-        constexpr int NG = KML_KM_GROUP;
-        int qs[NG];
-#pragma unroll
-        for (int u = 0; u < NG; ++u) {
-          qs[u] = need ? __builtin_ctzll(need) : -1;
-          need &= need - 1;
-        }
-        double2 v[NG];
-#pragma unroll
-        for (int u = 0; u < NG; ++u) v[u] = yy[min((qs[u] < 0 ? qs[0] : qs[u]) * 64 + lane, S - 1)];
-#pragma unroll
-        for (int u = 0; u < NG; ++u) {
-          if (qs[u] < 0) break;
-          const bool valid = qs[u] * 64 + lane < S;
-          bool m;
-          double g;
-          const bool dec = screen0<KC>(cl, v[u].x, v[u].y, m, g);
-          if (__ballot(valid && !dec))
-            if (valid && !dec) {  // tie band / range: the exact decision
-              m = member0_slow<KC>(cl, v[u].x, v[u].y);
-              g = 0.0;
-            }
-          // D + g / (2 Cmax), rounded down; past the float range a finite 2^127
-          const double td = (drift + g * inv2c) * (1.0 - 0x1p-20);
-          const float t = wave_min_f(valid ? (td < 0x1p127 ? (float)td : 0x1p127f) : INFINITY);
-          const uint64_t bits = __ballot(valid && m);
-          if (it == 0 || bits != lane_u64(wb, qs[u])) chg = 1;
-          if (lane == qs[u]) {
-            wb = bits;
-            wt = t;
+      while (need) {  // wave-uniform, one flagged word per pass
+        const int q = __builtin_ctzll(need);
+        need &= need - 1;
+        const double2 v = yy[min(q * 64 + lane, S - 1)];
+        const bool valid = q * 64 + lane < S;
+        bool m;
+        double g;
+        const bool dec = screen0<KC>(cl, v.x, v.y, m, g);
+        if (__ballot(valid && !dec))
+          if (valid && !dec) {  // tie band / range: the exact decision
+            m = member0_slow<KC>(cl, v.x, v.y);
+            g = 0.0;
           }
+        // D + g / (2 Cmax), rounded down; past the float range a finite 2^127
+        const double td = (drift + g * kc->inv2c) * (1.0 - 0x1p-20);
+        const float t = wave_min_f(valid ? (td < 0x1p127 ? (float)td : 0x1p127f) : INFINITY);
+        const uint64_t bits = __ballot(valid && m);
+        if (it == 0 || bits != lane_u64(wb, q)) chg = 1;
+        if (lane == q) {
+          wb = bits;
+          wt = t;
         }
         KM_COUNT(KS_WORDS, 1);
       }
@@ -1336,7 +1342,6 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
     KM_STAMP(KS_COMPACT);
     const int n = nmem;
     cnt += n;
-    const DdRcp yc = dd_rcp((double)cnt);  // the update's divisor, ahead of the sums
     if (n > L.cap) {  // more members than the list holds (degenerate input): straight from the words
       double acc = lane == 0 ? sr : si;  // lane 0: real chain, lane 1: imaginary chain, ascending j
       for (int w = 0; w < Sw; ++w) {
@@ -1348,7 +1353,8 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
       si = lane_d(acc, 1);
     } else if (scan) {
       int steps = 0;
-      ordered_sum_vals2(sr, si, vals, n, lane, steps);
+      sr = ordered_sum_vals1(sr, vals, 0, n, lane, steps);  // the real chain, then the imaginary one
+      si = ordered_sum_vals1(si, vals, 1, n, lane, steps);
       KM_COUNT(KS_STEPS, steps);
     } else {  // lane 0: real chain, lane 1: imaginary chain
       double acc = lane == 0 ? sr : si;
@@ -1359,8 +1365,14 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
     }
     KM_STAMP(KS_SUM);
     {
+      const DdRcp yc = dd_rcp((double)cnt);
       const cplx m0 = cdiv_count(sr, si, cnt, yc);  // kmeans.cc:59-62
-      hat = cdiv_const(m0, c0, c0k);                // kmeans.cc:64-71
+      CdivConst c0k;
+      c0k.ratio = kc->ratio;
+      c0k.denom = kc->denom;
+      c0k.yd = DdRcp{kc->yd_hi, kc->yd_lo, kc->yd_k};
+      c0k.mode = kc->mode;
+      hat = cdiv_const(m0, c0, c0k);  // kmeans.cc:64-71
     }
     KM_STAMP(KS_UPDATE);
   }
@@ -1384,8 +1396,11 @@ bool run_kmeans_wave(const double *cons, const double *rot, const double2 *y, in
                      double2 *h_hat, double2 *h4, double2 *hat_out, hipStream_t s, hipError_t &err) {
   const size_t lds = (size_t)kWaveWpg * km_wave_lds(S, KC).stride;
   if (S > 64 * kFusedMaxW || lds > 160 * 1024) return false;
+  // default: this kernel up to 16 points; 64QAM's 64-distance screens go to
+  // the two-wave kernel, which splits each codeword's words over two waves
+  // (PEG8064/64QAM, 4096 codewords: 0.64 vs 0.73 ms); KML_KMEANS=wave / fused forces
   const char *e = getenv("KML_KMEANS");
-  if (!e || e[0] != 'w') return false;  // KML_KMEANS=wave (A/B; the default is km_fused_kernel)
+  if (e ? e[0] != 'w' : KC > 16) return false;
   err = hipFuncSetAttribute((const void *)km_wave_kernel<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return true;
   int incremental = 1, scan = 1;

@@ -455,24 +455,24 @@ def test_kmeans_adversarial_ties(data_dir, modem):
         assert np.array_equal(hh[b], ref, equal_nan=True), b
 
 
-@pytest.mark.parametrize("mode", ["default", "sequential_sum", "owned_words", "wave", "wave_sequential_sum"])
+@pytest.mark.parametrize("mode", ["fused", "fused_sequential_sum", "fused_owned_words", "wave", "wave_sequential_sum"])
 @pytest.mark.parametrize("modem", ["2bits_QPSK.txt", "4bit_16QAM_Gray.txt", "6bits_64QAM_Gray.txt"])
 def test_kmeans_cumulative_sum_adversarial(data_dir, modem, mode, monkeypatch):
-    """The fused k-means' cumulative cluster-0 sums (kmeans.hip
-    ordered_sum_wave: binade-segmented grid scans, tie parities, binade exits)
-    and its incremental assignment against the oracle's sequential
-    kmeans.cc:33-46, on inputs built to hit their corner cases: noise on a
-    coarse dyadic grid (ties), a cluster-0 centre on an axis (sums that change
-    sign), tiny and huge channels (extreme binades; thresholds past the float
-    range), NaN / inf symbols (the complex products' infinity recovery) and
-    realistic frames; with the default kernel (two waves per codeword), its
-    two-lane sequential sums (KML_KM_SCAN=0) and each wave assigning its own
-    words (KML_KM_BAL=0), and the one-wave kernel (KML_KMEANS=wave: value
-    list in LDS, both chains per scan step) with and without its scans."""
+    """The k-means kernels' cumulative cluster-0 sums (kmeans.hip
+    ordered_sum_wave / ordered_sum_vals2: binade-segmented grid scans, tie
+    parities, binade exits) and their incremental assignment against the
+    oracle's sequential kmeans.cc:33-46, on inputs built to hit their corner
+    cases: noise on a coarse dyadic grid (ties), a cluster-0 centre on an axis
+    (sums that change sign), tiny and huge channels (extreme binades;
+    thresholds past the float range), NaN / inf symbols (the complex products'
+    infinity recovery) and realistic frames; with the two-wave kernel
+    (KML_KMEANS=fused), its two-lane sequential sums (KML_KM_SCAN=0) and each
+    wave assigning its own words (KML_KM_BAL=0), and the one-wave kernel
+    (KML_KMEANS=wave: value list in LDS, both chains per scan step) with and
+    without its scans."""
+    monkeypatch.setenv("KML_KMEANS", mode.split("_")[0])
     monkeypatch.setenv("KML_KM_SCAN", "0" if mode.endswith("sequential_sum") else "1")
-    monkeypatch.setenv("KML_KM_BAL", "0" if mode == "owned_words" else "1")
-    if mode.startswith("wave"):
-        monkeypatch.setenv("KML_KMEANS", "wave")
+    monkeypatch.setenv("KML_KM_BAL", "0" if mode.endswith("owned_words") else "1")
     matrix = "PEG8064regular0.5.txt" if "64QAM" in modem else "PEG2304regular0.5.txt"
     ctx = ctx_for(data_dir, matrix, modem, False)
     om = O.Modem(os.path.join(data_dir, modem))
