@@ -1136,7 +1136,14 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
 #ifndef KML_KM_CAPDIV
 #define KML_KM_CAPDIV 3
 #endif
-constexpr int kWaveWpg = 4;  // codewords (waves) per workgroup: independent, no barrier between them
+// Codewords (waves) per workgroup.  One: a workgroup's LDS is released when its
+// own codeword ends, not with the slowest of four (iteration counts vary), and
+// the dispatcher refills the CU per codeword: blind PEG2304 2.69 ms with four,
+// 2.59 with two, 2.44 with one (profiles/r05_ab5_summary.txt).
+#ifndef KML_KM_WPG
+#define KML_KM_WPG 1
+#endif
+constexpr int kWaveWpg = KML_KM_WPG;
 struct KmWaveLds {
   int cap, off_cl, stride;
 };
@@ -1165,8 +1172,10 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
   if (cw >= B) return;  // wave-uniform; the waves of a workgroup never wait for each other
   double2 *vals = reinterpret_cast<double2 *>(kmem + wave * L.stride);           // [cap] the members' symbols, in order
   double2 *cl = reinterpret_cast<double2 *>(kmem + wave * L.stride + L.off_cl);  // [KC] cluster points
-  volatile double2 *cs = cl + KC;                                                // [KC] constellation points
-  volatile KmWaveConst *kc = reinterpret_cast<volatile KmWaveConst *>(cl + 2 * KC);
+  // (plain LDS pointers: the loop's LDS stores may alias them, so the values
+  // are reloaded where used instead of being held in registers)
+  double2 *cs = cl + KC;                                              // [KC] constellation points
+  KmWaveConst *kc = reinterpret_cast<KmWaveConst *>(cl + 2 * KC);
   const int Sw = (S + 63) / 64;
 #if KML_STAMPS
   unsigned long long km_prev = __builtin_amdgcn_s_memtime();
@@ -1261,6 +1270,8 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
   // lane w < Sw: word w's membership bits and its threshold min(D(ref) + g / (2 Cmax)); -1: assign
   uint64_t wb = 0;
   float wt = -1.0f;
+  uint64_t wb_list = 0;  // lane w: word w's bits and list offset at the last rebuild
+  int excl_list = 0;
   const double *yv = reinterpret_cast<const double *>(yy);
   __builtin_amdgcn_wave_barrier();
   KM_STAMP(KS_PRO);
@@ -1324,16 +1335,29 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
       const int c = __popcll(wb);
       const int incl = wave_inclusive_scan_i(c);
       const int excl = incl - c;
+      // only the words whose members or list offset changed are rewritten (the
+      // others' segments hold their values already); all of them after an
+      // overflowing list (its tail was never written)
+      const bool full = it == 0 || nmem > L.cap;
+      uint64_t need = __ballot(lane < Sw && (full || wb != wb_list || excl != excl_list));
       nmem = __builtin_amdgcn_readlane(incl, 63);
-      for (int w0 = 0; w0 < Sw; w0 += 6) {  // six words' loads in flight
+      wb_list = wb;
+      excl_list = excl;
+      while (need) {  // wave-uniform, six words' loads in flight
+        int qs[6];
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+          qs[u] = need ? __builtin_ctzll(need) : -1;
+          need &= need - 1;
+        }
         double2 v[6];
 #pragma unroll
-        for (int u = 0; u < 6; ++u) v[u] = yy[min((w0 + u) * 64 + lane, S - 1)];  // past the last word: a repeat
+        for (int u = 0; u < 6; ++u) v[u] = yy[min((qs[u] < 0 ? qs[0] : qs[u]) * 64 + lane, S - 1)];
 #pragma unroll
         for (int u = 0; u < 6; ++u)
-          if (w0 + u < Sw) {
-            const uint64_t bits = lane_u64(wb, w0 + u);
-            const int p = __builtin_amdgcn_readlane(excl, w0 + u) + __popcll(bits & ((1ull << lane) - 1));
+          if (qs[u] >= 0) {
+            const uint64_t bits = lane_u64(wb, qs[u]);
+            const int p = __builtin_amdgcn_readlane(excl, qs[u]) + __popcll(bits & ((1ull << lane) - 1));
             if (((bits >> lane) & 1) && p < L.cap) vals[p] = v[u];
           }
       }
