@@ -48,7 +48,6 @@ struct GroupSync {
   unsigned bar;      // barrier arrivals (monotonic within a launch)
   unsigned flag[2];  // per iteration parity: bit 0 failing rows, bit 1 an unproven VN quotient
   unsigned cw;       // the group's current codeword (entry index)
-  unsigned nofast;   // some member saw a prior outside the FAST division domain
   unsigned errs;     // error bits of the codeword, summed over members
   unsigned pcnt;     // unsatisfied checks of the final hard decisions, summed
   unsigned xcc;      // bit per XCD a member runs on
@@ -1005,6 +1004,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
   __shared__ int sfail;                  // this member's early-stop flag (parity failures)
   __shared__ int sdead;                  // a tagged-exchange poll timed out: every wave leaves
   __shared__ int spcnt;                  // unsatisfied checks of the member's rows (tagged path)
+  __shared__ int snf;                    // this member saw a prior outside the FAST domain (barrier B's flag)
   unsigned nb = 0;                       // barrier sequence number (uniform, same on every member)
   unsigned g = 0;                        // global iteration counter of the tagged exchange (same on every member)
   if (a.B_dev && *a.B_dev == 0) return;  // nothing deferred: every workgroup leaves before the first barrier
@@ -1012,6 +1012,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
     bst[0] = bst[1] = bst[2] = bst[3] = 0;
     sfail = 0;
     sdead = 0;
+    snf = 0;
     const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
     __hip_atomic_fetch_or(&gs->xcc, 1u << xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1026,7 +1027,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
   for (;;) {
     if (member == 0 && tid == 0) {
       __hip_atomic_store(&gs->cw, atomicAdd(queue, 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&gs->nofast, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&gs->errs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&gs->pcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1051,10 +1051,17 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
     }
     // InitMsg: row slots and mirror slots (c2v = 0.5)
     for (int e = tid; e < nslots + kPartDummy; e += T) reinterpret_cast<double2 *>(smem)[e] = make_double2(0.5, 0.5);
-    if (__ballot(!ok) != 0 && (tid & 63) == 0)
-      __hip_atomic_fetch_or(&gs->nofast, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;
-    const bool fast = !EXACT && (fast_allowed & 1) && !ld_rlx(&gs->nofast);
+    // "some member holds a prior outside the FAST domain" travels as this
+    // barrier's flag count, which every thread of every member reads from the
+    // same arrivals.  (It was a group word that member 0 cleared at the top of
+    // the next codeword: after a deferred codeword, which has no closing
+    // barrier, that clear could land before a slower member's waves read the
+    // word, so members and waves disagreed on fast, took different paths and
+    // a group barrier timed out — tools/stress_part.py)
+    if (__ballot(!ok) != 0 && (tid & 63) == 0) atomicOr(&snf, 1);
+    const int nf = part_barrier<kG>(gs, bst, nb, same_xcd, abort, &snf);
+    if (nf < 0) return;
+    const bool fast = !EXACT && (fast_allowed & 1) && (nf & 0xFF) == 0;
     constexpr bool tagged = TAGGED;
 
     int iter = 0, pcnt = 0, decbuf = 0;
@@ -1083,7 +1090,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
                                                         dec, mb_v2c, mb_c2v, gc, c, vaddr, vpos, vact, pv, crow, cbase,
                                                         cact, xr, xc, odd, member, iter, conv, (fast_allowed & 2) != 0);
       if (st < 0) return;
-      if (st == 1) {  // group-wide: nofast, or the suspect count every member read at the same barrier
+      if (st == 1) {  // group-wide: not FAST, or the suspect count every member read at the same barrier
         if (member == 0 && tid == 0) {
           a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = cw;
           if (fast && a.counters) atomicAdd(&a.counters[CNT_REDONE], 1ull);

@@ -612,6 +612,30 @@ def test_partitioned_kernel_tagged_exchange_and_deferral(data_dir, monkeypatch, 
     ctx.close()
 
 
+def test_partitioned_kernel_deferral_liveness(data_dir, monkeypatch):
+    """Liveness of the partitioned kernel around deferred codewords: 150 rounds
+    of the decodes above (FAST codewords beside two deferred ones, budgets 20, 1
+    and 0, batches of 300, 1024 and 4096) never abort.  Before the not-FAST
+    vote travelled through the group barrier's flag count, member 0 cleared a
+    group word after a deferred codeword that a slower member might not have
+    read yet; the members then took different paths and a group barrier timed
+    out (tools/stress_part.py: the 42nd round)."""
+    monkeypatch.setenv("KML_PART_TAGGED", "1")
+    ctx = K.Context(matrix_file=os.path.join(data_dir, "PEG8064regular0.5.txt"),
+                    modem_file=os.path.join(data_dir, "6bits_64QAM_Gray.txt"), is5g=False, active=True,
+                    max_iter=20, device=0)
+    assert ctx.dims["part_group"] == 4
+    rng = np.random.default_rng(33)
+    for r in range(150):
+        B = (300, 1024, 4096)[r % 3]
+        p0 = np.clip(rng.normal(0.5, 0.28, (B, ctx.cc_len)), 0.02, 0.98)
+        p0[7, ::5] = -0.0
+        p0[23, 1::7] = 5e-320
+        for it in (20, 1, 0):
+            ctx.bp_decode(p0, iter_count=it, cc_hat=True, syn=np.zeros((B, ctx.M)))
+    ctx.close()
+
+
 @pytest.mark.parametrize("matrix,modem,is5g,max_iter", CODES)
 def test_empty_and_ragged_batches(data_dir, matrix, modem, is5g, max_iter):
     ctx = ctx_for(data_dir, matrix, modem, is5g, max_iter)
