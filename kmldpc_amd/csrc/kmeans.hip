@@ -655,6 +655,17 @@ __device__ __forceinline__ double ordered_sum_vals1(double acc, const double2 *v
   return acc;
 }
 
+// An upper bound of the Euclidean norm sqrt(a^2 + b^2): the fp64 form (at most
+// a few ulps off, v_sqrt_f64 included) times 1 + 1e-14, or |a| + |b| where a
+// square could under- or overflow (and for NaN input, NaN as before).  The
+// drift bound of the incremental assignment takes |c_k| and |hatH' - hatH| in
+// this norm (round 4 took |re| + |im| for both: up to 2x looser for QPSK).
+__device__ __forceinline__ double norm2_up(double a, double b) {
+  const double m = fmax(fabs(a), fabs(b));
+  if (!(m >= 0x1p-500 && m <= 0x1p500)) return fabs(a) + fabs(b);
+  return sqrt(a * a + b * b) * (1.0 + 1e-14);
+}
+
 // Lower bound of |sqrt(hi) - sqrt(lo)| (true distances of the fp cluster
 // points) from the screened squared distances lo <= hi:
 //   sqrt(hi) - sqrt(lo) = (hi - lo) / (sqrt(hi) + sqrt(lo)) >= (hi - lo) / (2 sqrt(hi)).
@@ -908,9 +919,9 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
   const cplx c0{cons[0], cons[1]};
   const CdivConst c0k = cdiv_prepare(c0);
   cplx hat = kml_cdiv(cplx{ys[mi].x, ys[mi].y}, c0);  // kmeans.cc:25
-  // 1 / (2 Cmax), rounded down (|c| <= |re| + |im|)
+  // 1 / (2 Cmax), rounded down (Cmax >= max |c_k|, norm2_up)
   double cb = 0.0;
-  for (int k = 0; k < KC; ++k) cb = fmax(cb, fabs(cons[2 * k]) + fabs(cons[2 * k + 1]));
+  for (int k = 0; k < KC; ++k) cb = fmax(cb, norm2_up(cons[2 * k], cons[2 * k + 1]));
   const double inv2c = cb > 0.0 ? (0.5 / cb) * (1.0 - 1e-12) : 0.0;
   // lane k < KC: cluster k of the previous iteration (tempClusters, zero at first)
   cplx prevk{0.0, 0.0};
@@ -943,7 +954,7 @@ __global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8
     KM_COUNT(KS_ITERS, 1);
     // drift bound D (rounded up), identical in every thread
     {
-      const double dd = (fabs(hat.re - hprev.re) + fabs(hat.im - hprev.im)) * (1.0 + 1e-15) +
+      const double dd = norm2_up(hat.re - hprev.re, hat.im - hprev.im) +
                         0x1p-48 * (fabs(hat.re) + fabs(hat.im) + fabs(hprev.re) + fabs(hprev.im));
       drift = (drift + dd) * (1.0 + 0x1p-50);
       hprev = hat;
@@ -1246,9 +1257,9 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
   cplx hat = kml_cdiv(cplx{yy[mi].x, yy[mi].y}, c0);  // kmeans.cc:25
   {
     const CdivConst c0k = cdiv_prepare(c0);
-    // 1 / (2 Cmax), rounded down (|c| <= |re| + |im|)
+    // 1 / (2 Cmax), rounded down (Cmax >= max |c_k|, norm2_up)
     double cb = 0.0;
-    for (int k = 0; k < KC; ++k) cb = fmax(cb, fabs(cons[2 * k]) + fabs(cons[2 * k + 1]));
+    for (int k = 0; k < KC; ++k) cb = fmax(cb, norm2_up(cons[2 * k], cons[2 * k + 1]));
     if (lane == 0) {
       kc->ratio = c0k.ratio;
       kc->denom = c0k.denom;
@@ -1294,7 +1305,7 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
     }
     KM_COUNT(KS_ITERS, 1);
     {
-      const double dd = (fabs(hat.re - hprev.re) + fabs(hat.im - hprev.im)) * (1.0 + 1e-15) +
+      const double dd = norm2_up(hat.re - hprev.re, hat.im - hprev.im) +
                         0x1p-48 * (fabs(hat.re) + fabs(hat.im) + fabs(hprev.re) + fabs(hprev.im));
       drift = (drift + dd) * (1.0 + 0x1p-50);
       hprev = hat;
