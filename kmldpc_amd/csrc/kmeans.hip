@@ -15,7 +15,7 @@
 // has to decide, per symbol, whether cluster 0 is the FIRST minimum of the K
 // distances (kmeans.cc:41-44).
 //
-// MI355X mapping.  The production path is km_fused_kernel (one workgroup per
+// MI355X mapping.  The production path is km_wave_kernel (one wave per
 // codeword, the whole Run in one launch; described at its definition).  The
 // two-launch form below (KML_KMEANS=split, A/B and S > 4096) runs one k-means
 // iteration as two launches:
@@ -249,21 +249,9 @@ __global__ void km_final_kernel(const double *__restrict__ cons, const double *_
 }
 
 // ---------------------------------------------------------------------------
-// Fused k-means: one workgroup of two waves per codeword runs the whole
-// KMeans::Run.  The symbols are staged in LDS once; each iteration assigns in
-// parallel (same screening as km_assign, 64-symbol words by ballot), lists the
-// cluster-0 members' indices in ascending symbol order (u16, LDS), and sums
-// their values onto the cumulative sum in that order (the reference's
-// sequential rounding: wave 0 the real chain, wave 1 the imaginary chain, by
-// exact binade-segmented scans, ordered_sum_wave); lane 0 then updates h_hat.
-// y is read from HBM once; LDS per codeword is 16 S + S bytes + 12 per word
-// (km_lds), so 8 codewords share a CU for QPSK/PEG2304 (7 with the full-length
-// member list: 3.65 -> see DESIGN.md).
-//
-// Per-iteration latency is what bounds this kernel (each codeword is a chain
-// of dependent steps; a dependent VALU step costs ~40 cycles with 3-4 waves
-// per SIMD), so the iterations skip the work whose outcome is already known,
-// exactly:
+// The whole KMeans::Run in one launch (km_wave_kernel, below).  Each codeword
+// is a chain of dependent iterations, so the iterations skip the work whose
+// outcome is already known, exactly:
 //   * convergence (kmeans.cc:47-56) compares clusters_ = c_k * hatH with the
 //     previous iteration's; lanes k < KC compute both at the iteration START
 //     (the cluster points the assignment needs anyway), so a converged
@@ -275,40 +263,20 @@ __global__ void km_final_kernel(const double *__restrict__ cons, const double *_
 //     squared distances and of glibc hypot folded in).  A later hatH moves
 //     cluster k by at most |c_k| |hatH' - hatH| plus the rounding of the two
 //     complex products, so while 2 Cmax (D(t) - D(ref)) < g — D the running
-//     sum of the per-iteration bounds |dh| + 2^-48 (|h| + |h'|), rounded up —
-//     the symbol's decision cannot change.  A 64-symbol word is re-assigned
-//     when any of its symbols may have changed: each word keeps the minimum
-//     over its symbols of T = D(ref) + g / (2 Cmax) (float, rounded down);
-//   * the member list is rebuilt only when some word's membership bits
-//     changed (each wave scans the word popcounts itself and scatters its own
-//     words: no barrier in between);
+//     sum of the per-iteration bounds |dh| + 2^-48 (|h| + |h'|), rounded up,
+//     norms by norm2_up — the symbol's decision cannot change.  A 64-symbol
+//     word is re-assigned when any of its symbols may have changed: each word
+//     keeps the minimum over its symbols of T = D(ref) + g / (2 Cmax) (float,
+//     rounded down);
+//   * the members' list is rebuilt only when some word's membership bits
+//     changed, and then only the words whose members or offset changed;
 //   * the cumulative-mean division by (cnt, 0) and the division by c[0] take
 //     __divdc3's own branch with the constant parts hoisted (exact: same
 //     operations on the same values).
-// Measured (MI355X, 32768 PEG2304/QPSK codewords at Es/N0 2 dB, 19.9
-// iterations each): 4.28 ms -> 3.31 ms; tools/km_stamps.py gives the phases.
-constexpr int kFusedT = 128;  // two waves per codeword (the two sum chains), up to 7 codewords per CU (LDS)
-constexpr int kFusedMaxW = 64;  // 64-symbol words: S <= 4096
-// Dynamic LDS of one codeword: the symbols [S] double2, the compacted member
-// list [cap + 24] u16 (cap = S/2 rounded up to 8: cluster 0 of a constellation
-// of >= 2 points; a larger cluster, seen only on degenerate inputs, is summed
-// straight from the membership words), the membership words [2][Sw] u64 and
-// their drift thresholds [2][Sw] float, both double-buffered by iteration
-// parity (a wave still in iteration i reads buffer i & 1 while the other
-// wave's assignment of i + 1 writes the other one).  PEG2304/QPSK: 20,488
-// bytes + ~120 static, so 8 codewords share a CU (the 16 KB register budget of
-// 4 waves per SIMD allows 8).
-struct KmLds {
-  int cap, off_mem, off_wbits, off_wthr, bytes;
-};
-__host__ __device__ constexpr KmLds km_lds(int S) {
-  const int cap = ((S + 1) / 2 + 7) & ~7;
-  const int Sw = (S + 63) / 64;
-  const int off_mem = 16 * S;
-  const int off_wbits = (off_mem + 2 * (cap + 24) + 7) & ~7;
-  const int off_wthr = off_wbits + 16 * Sw;
-  return KmLds{cap, off_mem, off_wbits, off_wthr, off_wthr + 8 * Sw};
-}
+// Round 4's two-wave form (km_fused_kernel: y staged in LDS, two waves per
+// codeword, 8 per CU) ran 3.50 ms per 32768 PEG2304/QPSK codewords; the
+// one-wave kernel runs 2.39 ms and took 64QAM over too.
+constexpr int kMaxS = 4096;  // 64-symbol words in the lanes of one wave
 
 // Phase timing (stamps build, -DKML_STAMPS=1; tools/km_stamps.py): thread 0's
 // s_memtime deltas summed over workgroups, plus event counts.
@@ -377,50 +345,6 @@ __device__ __forceinline__ float wave_min_f(float v) {
   v = dpp_min_step<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
   v = dpp_min_step<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-
-// acc + y[2 m_0] + y[2 m_1] + ... + y[2 m_(n-1)] in that order (the
-// reference's rounding), m the compacted member indices (u16, 16-byte
-// aligned, at least n + 24 readable; indices past n are clamped into [0, S)).
-// Software pipeline over blocks of 8: the indices of block b + 2 and the
-// values of block b + 1 (from indices already in registers) are in flight
-// while block b is added, so neither LDS latency sits on the chain of
-// dependent adds.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void fetch8(const double *yv, u32x4 q, int S, double (&v)[8]) {
-  const unsigned w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    v[2 * k] = yv[2 * min((int)(w[k] & 0xffffu), S - 1)];
-    v[2 * k + 1] = yv[2 * min((int)(w[k] >> 16), S - 1)];
-  }
-}
-__device__ __forceinline__ double ordered_sum(double acc, const double *yv, const unsigned short *m, int n, int S) {
-  // The index list is the same for both lanes; left uniform, hipcc moves the
-  // indices to SGPRs (v_readfirstlane) right after their loads, which waits
-  // for them on the spot.  A VGPR base address keeps them in VGPRs, waited
-  // for only where the values' addresses are formed, a block later.
-  unsigned mb = lds_addr(m);
-  asm volatile("" : "+v"(mb));
-  double cur[8];
-  fetch8(yv, lds_ld<u32x4>(mb), S, cur);
-  u32x4 qn = lds_ld<u32x4>(mb + 16);
-  int i = 0;
-#pragma clang loop unroll(disable)  // unrolled, the second copy waits for the first copy's index load
-  for (; i + 8 <= n; i += 8) {
-    const u32x4 q2 = lds_ld<u32x4>(mb + 2 * i + 32);
-    double nxt[8];
-    fetch8(yv, qn, S, nxt);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc = acc + cur[k];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
-    qn = q2;
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k)  // the tail (< 8 values), already loaded
-    if (i + k < n) acc = acc + cur[k];
-  return acc;
 }
 
 // The same sum computed by a whole wave (binade-segmented integer scans;
@@ -602,31 +526,6 @@ __device__ __forceinline__ double seq_run(double acc, const double (&x)[kScanPer
 }
 __device__ __forceinline__ bool scan_ok(double acc, int seq) { return seq == 0 && acc != 0.0 && isfinite(acc); }
 
-__device__ __forceinline__ double ordered_sum_wave(double acc, const double *yv, const unsigned short *m, int n, int S,
-                                                   int lane, int &steps) {
-  int i = 0, seq = 0;
-  while (i < n) {  // wave-uniform
-    ++steps;
-    const int c = min(64 * kScanPer, n - i);
-    double x[kScanPer];
-#pragma unroll
-    for (int k = 0; k < kScanPer; ++k) {
-      const int j = i + kScanPer * lane + k;
-      x[k] = j < n ? yv[2 * min((int)m[j], S - 1)] : 0.0;
-    }
-    int adv;
-    if (!scan_ok(acc, seq)) {
-      acc = seq_run(acc, x, c, adv, seq);
-    } else {
-      ScanStep st;
-      scan_a(acc, x, c, lane, st);
-      acc = scan_b(st, x, c, lane, adv, seq);
-    }
-    i += adv;
-  }
-  return acc;
-}
-
 // One chain (comp 0: real, 1: imaginary) over the LDS value list.
 __device__ __forceinline__ double ordered_sum_vals1(double acc, const double2 *vals, int comp, int n, int lane,
                                                     int &steps) {
@@ -667,19 +566,13 @@ __device__ __forceinline__ double norm2_up(double a, double b) {
 }
 
 // Lower bound of |sqrt(hi) - sqrt(lo)| (true distances of the fp cluster
-// points) from the screened squared distances lo <= hi:
+// points) from the screened squared distances lo <= hi (screen0):
 //   sqrt(hi) - sqrt(lo) = (hi - lo) / (sqrt(hi) + sqrt(lo)) >= (hi - lo) / (2 sqrt(hi)).
 // The fp64 d2 values are within 2^-50 relative of the exact squares, hence
 // the 1e-13 (hi + lo) term; the float conversion and v_rsq_f32 are within
 // 2^-22 relative, hence 0.5 (1 - 1e-5); the final 1e-13 (hi + 1) >= 2e-13
 // sqrt(hi) term absorbs glibc hypot's rounding at the later comparison.
 // 0 outside the float range (the symbol is then re-assigned every iteration).
-__device__ __forceinline__ double dist_margin(double lo, double hi) {
-  if (!(lo >= 1e-30 && hi <= 1e30)) return 0.0;
-  const double num = (hi - lo) - 1e-13 * (hi + lo);
-  const double q = num * (double)__builtin_amdgcn_rsqf((float)hi) * (0.5 * (1.0 - 1e-5)) - 1e-13 * (hi + 1.0);
-  return q > 0.0 ? q : 0.0;
-}
 
 // the tie-band / exact decision out of line (rare; keeps the hot loop's
 // registers free)
@@ -696,44 +589,13 @@ __device__ KM_SLOW bool member0_slow(const double2 *cl, double yr, double yi) {
   return member0<KC>(cl, yr, yi);
 }
 
-// member0 (above) plus the decision's margin g (0 when the tie band or the
-// exact path decided).
-template <int KC>
-__device__ __forceinline__ bool member0_margin(const double2 *cl, double yr, double yi, double &g) {
-  double d0 = 0.0, m1 = 0.0;
-  bool fin = true;
-#pragma unroll 8
-  for (int k = 0; k < KC; ++k) {
-    const double2 c = cl[k];
-    const double dr = c.x - yr, di = c.y - yi;
-    const double d = dr * dr + di * di;
-    if (k == 0)
-      d0 = d;
-    else if (k == 1 || d < m1)
-      m1 = d;
-    fin = fin && d2_ok(d);
-  }
-  g = 0.0;
-  if (fin) {
-    if (d0 < m1 * (1.0 - kTieBand)) {
-      g = dist_margin(d0, m1);
-      return true;
-    }
-    if (d0 > m1 * (1.0 + kTieBand)) {
-      g = dist_margin(m1, d0);
-      return false;
-    }
-  }
-  return member0_slow<KC>(cl, yr, yi);
-}
-
-// member0_margin's fast path without branches (the one-wave kernel): returns
-// whether the screen decided; then m is the decision and g its margin, else
-// the caller runs member0_slow (g = 0).  The range test d2_ok of every
+// The assignment's screen, branch-free: returns whether it decided; then m is
+// "cluster 0 is the first minimum" (member0) and g its margin (the bound
+// above), else the caller runs member0_slow (g = 0).  The range test d2_ok of every
 // distance is taken on the high dwords as unsigned integers (NaN and inf
 // included): hi(d) > hi(1e-290) and hi(d) < hi(1e290) imply 1e-290 < d <
-// 1e290, so the screen decides only where member0_margin does, with the same
-// operations on the same values (elsewhere the exact decision, with g = 0).
+// 1e290, so the screen decides only where member0's screen does, with the
+// same operations on the same values (elsewhere the exact decision, g = 0).
 constexpr unsigned kD2HiLo = 0x03b8f2b0u;  // high dword of 1e-290
 constexpr unsigned kD2HiHi = 0x7c2485ceu;  // high dword of 1e290
 template <int KC>
@@ -821,326 +683,19 @@ __device__ __forceinline__ cplx cdiv_const(cplx n, cplx dd, const CdivConst &k) 
   return cplx{x, y};
 }
 
-// four waves per SIMD (<= 128 registers): 7 codewords per CU fit the LDS, and
-// at 129+ registers only 6 do (QPSK: 3.3 -> 4.1 ms when the exact division's
-// registers pushed it past)
-template <int KC>
-__global__ __launch_bounds__(kFusedT) __attribute__((amdgpu_waves_per_eu(KC == 8 ? 1 : 4))) void km_fused_kernel(const double *__restrict__ cons,
-                                                           const double *__restrict__ rot,
-                                                           const double2 *__restrict__ y, int S, int iters,
-                                                           double2 *__restrict__ h_hat, double2 *__restrict__ h4,
-                                                           double2 *__restrict__ hat_out, int incremental, int scan, int bal) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char kmem[];
-  const KmLds L = km_lds(S);
-  double2 *ys = reinterpret_cast<double2 *>(kmem);  // [S] symbols
-  // compacted cluster-0 member indices, ascending: [cap + 24], 16-byte aligned
-  unsigned short *mem = reinterpret_cast<unsigned short *>(kmem + L.off_mem);
-  uint64_t *wbits = reinterpret_cast<uint64_t *>(kmem + L.off_wbits);  // [2][Sw] membership words
-  float *wthr = reinterpret_cast<float *>(kmem + L.off_wthr);  // [2][Sw] per word: min over its symbols of D(ref) + g / (2 Cmax)
-  __shared__ double2 clw[kFusedT / 64][KC];  // each wave's own copy of the clusters (no barrier)
-  __shared__ double red_d[kFusedT / 64];
-  __shared__ int red_i[kFusedT / 64];
-  __shared__ int s_exact;
-  __shared__ int s_flag[1 + kFusedT / 64];  // converged; per wave: member bits changed
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int NW = kFusedT / 64;
-  const int cw = blockIdx.x;
-  const int Sw = (S + 63) / 64;
-#if KML_STAMPS
-  unsigned long long km_prev = __builtin_amdgcn_s_memtime();
-  unsigned long long km_acc[KS_STEPS + 1] = {};
-  KM_COUNT(KS_CW, 1);
-#endif
-  const double2 *yy = y + (long long)cw * S;
-  for (int j = tid; j < S; j += kFusedT) ys[j] = yy[j];
-  if (tid == 0) s_exact = 0;
-  // every word is assigned in the first iteration (set before the prologue's
-  // barriers: the iterations have none before their first assignment)
-  if (tid < 2 * Sw) wthr[tid] = -1.0f;
-  __syncthreads();
-
-  // ---- first max |y| (kmeans.cc:17-22), screened like first_max_abs
-  double best = -1.0;
-  bool ex = false;
-  for (int j = tid; j < S; j += kFusedT) {
-    const double2 v = ys[j];
-    const double d = v.x * v.x + v.y * v.y;
-    if (!d2_ok(d) && !(d == 0.0)) ex = true;
-    if (d > best) best = d;
-  }
-  best = wave_max(best);
-  const bool wex = __ballot(ex) != 0;
-  if (lane == 0) {
-    red_d[wave] = best;
-    if (wex) s_exact = 1;
-  }
-  __syncthreads();
-  best = red_d[0];
-  for (int w = 1; w < NW; ++w) best = fmax(best, red_d[w]);
-  int mi;
-  if (!s_exact && best > 0.0) {
-    double hb = -1.0;  // max exact |y| among the band's candidates
-    for (int j = tid; j < S; j += kFusedT) {
-      const double2 v = ys[j];
-      if (v.x * v.x + v.y * v.y >= best * (1.0 - kTieBand)) hb = fmax(hb, kml_hypot(v.x, v.y));
-    }
-    hb = wave_max(hb);
-    __syncthreads();
-    if (lane == 0) red_d[wave] = hb;
-    __syncthreads();
-    hb = red_d[0];
-    for (int w = 1; w < NW; ++w) hb = fmax(hb, red_d[w]);
-    int jm = 0x7fffffff;  // the first index attaining it
-    for (int j = tid; j < S; j += kFusedT) {
-      const double2 v = ys[j];
-      if (v.x * v.x + v.y * v.y >= best * (1.0 - kTieBand) && kml_hypot(v.x, v.y) == hb) jm = min(jm, j);
-    }
-    jm = wave_min_i(jm);
-    if (lane == 0) red_i[wave] = jm;
-    __syncthreads();
-    mi = red_i[0];
-    for (int w = 1; w < NW; ++w) mi = min(mi, red_i[w]);
-  } else {  // the reference loop, sequentially (non-finite / extreme / all-zero input)
-    if (tid == 0) {
-      int m = 0;
-      double h0 = kml_hypot(ys[0].x, ys[0].y);
-      for (int j = 1; j < S; ++j) {
-        const double h = kml_hypot(ys[j].x, ys[j].y);
-        if (h0 < h) {
-          h0 = h;
-          m = j;
-        }
-      }
-      red_i[0] = m;
-    }
-    __syncthreads();
-    mi = red_i[0];
-  }
-  const cplx c0{cons[0], cons[1]};
-  const CdivConst c0k = cdiv_prepare(c0);
-  cplx hat = kml_cdiv(cplx{ys[mi].x, ys[mi].y}, c0);  // kmeans.cc:25
-  // 1 / (2 Cmax), rounded down (Cmax >= max |c_k|, norm2_up)
-  double cb = 0.0;
-  for (int k = 0; k < KC; ++k) cb = fmax(cb, norm2_up(cons[2 * k], cons[2 * k + 1]));
-  const double inv2c = cb > 0.0 ? (0.5 / cb) * (1.0 - 1e-12) : 0.0;
-  // lane k < KC: cluster k of the previous iteration (tempClusters, zero at first)
-  cplx prevk{0.0, 0.0};
-  cplx hprev = hat;
-  double drift = 0.0;  // D: the same value in every thread
-  double sr = 0.0, si = 0.0;  // cumulative cluster-0 sum (kmeans.cc:33-34, 46)
-  int cnt = 0;
-  int nmem = 0;  // members in the current list
-  KM_STAMP(KS_PRO);
-  for (int it = 0; it < iters; ++it) {
-    // clusters_[k] = c[k] * hatH, and the convergence test against
-    // tempClusters (kmeans.cc:26-28 / 72-74, 47-56)
-    // Both waves compute the clusters and the test (KC <= 64: lanes k < KC) on
-    // the same hatH, into their own copies: the same values, no barrier.
-    double2 *cl = clw[wave];
-    int conv;
-    {
-      bool same = true;
-      if (lane < KC) {
-        const cplx p = kml_cmul(cplx{cons[2 * lane], cons[2 * lane + 1]}, hat);
-        cl[lane] = make_double2(p.re, p.im);
-        same = (p.re == prevk.re) && (p.im == prevk.im);
-        prevk = p;
-      }
-      conv = __ballot(!same) == 0;
-      __builtin_amdgcn_wave_barrier();  // the wave's cluster stores precede its loads below (LDS in order per wave)
-    }
-    KM_STAMP(KS_CLUSTERS);
-    if (conv) break;  // the reference breaks after an assignment it then discards
-    KM_COUNT(KS_ITERS, 1);
-    // drift bound D (rounded up), identical in every thread
-    {
-      const double dd = norm2_up(hat.re - hprev.re, hat.im - hprev.im) +
-                        0x1p-48 * (fabs(hat.re) + fabs(hat.im) + fabs(hprev.re) + fabs(hprev.im));
-      drift = (drift + dd) * (1.0 + 0x1p-50);
-      hprev = hat;
-    }
-    uint64_t *cur = wbits + (it & 1) * Sw;
-    const uint64_t *prv = wbits + ((it & 1) ^ 1) * Sw;
-    float *tcur = wthr + (it & 1) * Sw;
-    const float *tprv = wthr + ((it & 1) ^ 1) * Sw;
-    // assignment: is cluster 0 the first minimum?  (kmeans.cc:36-46), only
-    // the words whose decisions the drift may have changed; the others keep
-    // the previous iteration's bits and thresholds
-    int chg = 0;
-    {
-      uint64_t need;  // this wave's flagged words (bal: bit = word; else bit q = word wave + NW q)
-      uint64_t oldb;  // lane l: the previous bits of word l (bal) or of word wave + NW l
-      if (bal) {
-        // both waves test every word (lane = word) and take the flagged words
-        // by rank: wave v the ranks v, v + NW, ... (balanced whatever their
-        // indices); unflagged words are copied by their index's wave
-        const bool inw = lane < Sw;
-        oldb = inw ? prv[lane] : 0ull;
-        const bool nd = inw && (!incremental || !(drift < (double)tprv[lane]));
-        if (inw && !nd && lane % NW == wave) {
-          cur[lane] = oldb;
-          tcur[lane] = tprv[lane];
-        }
-        need = 0;
-        int k = 0;
-        for (uint64_t b = __ballot(nd); b; b &= b - 1, ++k)
-          if (k % NW == wave) need |= b & (~b + 1);
-      } else {
-        // this wave's words w = wave + NW q: lane q tests word q's threshold
-        const int nq = (Sw - wave + NW - 1) / NW;  // <= 64 (S <= 4096)
-        const int wl = wave + NW * lane;
-        const bool own = lane < nq;
-        oldb = own ? prv[wl] : 0ull;
-        const bool needq = own && (!incremental || !(drift < (double)tprv[wl]));
-        if (own && !needq) {
-          cur[wl] = oldb;
-          tcur[wl] = tprv[wl];
-        }
-        need = __ballot(needq);
-      }
-      auto widx = [&](int q) { return bal ? q : wave + NW * q; };
-      // two flagged words per pass: their LDS loads, distance screens and
-      // wave minima are independent chains that overlap
-      auto word = [&](int q, bool &m, float &t) {
-        const int j = widx(q) * 64 + lane;
-        m = false;
-        t = INFINITY;
-        if (j < S) {
-          double g;
-          m = member0_margin<KC>(cl, ys[j].x, ys[j].y, g);
-          // D + g / (2 Cmax), rounded down; past the float range a finite 2^127
-          // (an infinite threshold would never let the word be re-assigned)
-          const double td = (drift + g * inv2c) * (1.0 - 0x1p-20);
-          t = td < 0x1p127 ? (float)td : 0x1p127f;
-        }
-      };
-      auto commit = [&](int q, bool m, float t) {
-        const int w = widx(q);
-        const uint64_t bits = __ballot(m);
-        if (it == 0 || bits != lane_u64(oldb, q)) chg = 1;
-        if (lane == 0) {
-          cur[w] = bits;
-          tcur[w] = t;
-        }
-      };
-      while (need) {  // wave-uniform
-        const int q1 = __builtin_ctzll(need);
-        need &= need - 1;
-        if (need) {
-          const int q2 = __builtin_ctzll(need);
-          need &= need - 1;
-          bool m1, m2;
-          float t1, t2;
-          word(q1, m1, t1);
-          word(q2, m2, t2);
-          t1 = wave_min_f(t1);
-          t2 = wave_min_f(t2);
-          commit(q1, m1, t1);
-          commit(q2, m2, t2);
-        } else {
-          bool m1;
-          float t1;
-          word(q1, m1, t1);
-          commit(q1, m1, wave_min_f(t1));
-        }
-#if KML_STAMPS
-        if (tid == 0) km_acc[KS_WORDS] += 1;  // wave 0's passes; x NW at the flush (an estimate)
-#endif
-      }
-    }
-    if (lane == 0) s_flag[1 + wave] = chg;
-    __syncthreads();
-    int rebuild = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) rebuild |= s_flag[1 + w];
-    KM_STAMP(KS_ASSIGN);
-    if (rebuild) {  // member list changed: rebuild it
-      KM_COUNT(KS_COMPACTIONS, 1);
-      // every wave computes the word offsets itself (exclusive prefix of the
-      // popcounts, DPP scan over lanes = words, Sw <= 64) and scatters its own
-      // words' members: no barrier between the two
-      const uint64_t bl = lane < Sw ? cur[lane] : 0ull;
-      const int c = __popcll(bl);
-      const int incl = wave_inclusive_scan_i(c);
-      const int excl = incl - c;
-      nmem = __builtin_amdgcn_readlane(incl, 63);
-      for (int w = wave; w < Sw; w += NW) {
-        const uint64_t bits = ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(bl >> 32), w) << 32) |
-                              (unsigned)__builtin_amdgcn_readlane((int)bl, w);
-        if ((bits >> lane) & 1) {
-          const int p = __builtin_amdgcn_readlane(excl, w) + __popcll(bits & ((1ull << lane) - 1));
-          if (p < L.cap) mem[p] = (unsigned short)(w * 64 + lane);
-        }
-      }
-      __syncthreads();
-    }
-    KM_STAMP(KS_COMPACT);
-    const int n = nmem;
-    cnt += n;
-    const DdRcp yc = dd_rcp((double)cnt);  // the update's divisor, ahead of the sums
-    if (n > L.cap) {  // more members than the list holds (degenerate input): straight from the words
-      if (tid < 2) {  // lane 0: real chain, lane 1: imaginary chain, ascending j
-        double acc = tid == 0 ? sr : si;
-        const double *yv = reinterpret_cast<const double *>(ys) + tid;
-        for (int w = 0; w < Sw; ++w)
-          for (uint64_t b = cur[w]; b; b &= b - 1) acc = acc + yv[2 * (w * 64 + __builtin_ctzll(b))];
-        red_d[tid] = acc;
-      }
-    } else if (scan) {  // wave 0: the real chain, wave 1: the imaginary chain (kFusedT = 128)
-      int steps = 0;
-      const double acc = ordered_sum_wave(wave == 0 ? sr : si, reinterpret_cast<const double *>(ys) + wave, mem, n, S,
-                                          lane, steps);
-      KM_COUNT(KS_STEPS, steps);
-      if (lane == 0) red_d[wave] = acc;
-    } else if (tid < 2) {  // lane 0: real chain, lane 1: imaginary chain, ascending j
-      red_d[tid] = ordered_sum(tid == 0 ? sr : si, reinterpret_cast<const double *>(ys) + tid, mem, n, S);
-    }
-    __syncthreads();
-    sr = red_d[0];
-    si = red_d[1];
-    KM_STAMP(KS_SUM);
-    // every lane of both waves updates hatH (the same operations on the same
-    // values, kmeans.cc:59-71): no broadcast, no barrier
-    {
-      const cplx m0 = cdiv_count(sr, si, cnt, yc);  // kmeans.cc:59-62
-      const cplx nh = cdiv_const(m0, c0, c0k);  // kmeans.cc:64-71
-      hat = nh;
-    }
-    KM_STAMP(KS_UPDATE);
-  }
-#if KML_STAMPS
-  if (tid == 0) {
-    km_acc[KS_WORDS] *= NW;
-    for (int i = 0; i <= KS_STEPS; ++i) atomicAdd(&kml_km_stamps[i], km_acc[i]);
-  }
-#endif
-  if (tid == 0) {
-    if (hat_out) hat_out[cw] = make_double2(hat.re, hat.im);  // the final hatH (clusters_ = c[k] * hatH)
-    const cplx hh = kml_cdiv(kml_cmul(c0, hat), c0);  // simulator.cc:145
-    h_hat[cw] = make_double2(hh.re, hh.im);
-    for (int j = 0; j < 4; ++j) {  // simulator.cc:146-148
-      const cplx r = kml_cmul(hh, cplx{rot[2 * j], rot[2 * j + 1]});
-      h4[(long long)cw * 4 + j] = make_double2(r.re, r.im);
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
-// One wave per codeword (the production k-means).  The fused kernel above is
-// capped at 8 codewords per CU by its LDS copy of the symbols (16 S bytes) and
-// by its two 116-register waves, and each codeword is a chain of dependent
-// steps: the kernel runs at the latency of that chain times the number of
-// codeword rounds (19.9 iterations x ~26 K cycles, 18 % VALU busy).  Here a
-// codeword is one wave with no LDS copy of y: the symbols are read where they
-// lie (HBM, then L2 / Infinity Cache for the iterations' re-reads: coalesced
-// 64-symbol words for the assignment, a gather of the listed members for the
-// sums); a word's membership bits and drift threshold live in the registers of
-// lane = word (S <= 4096); LDS holds only the member index list and the
-// cluster points, ~1.3 KB per codeword.  Residency is then set by registers
-// (<= 128: 16 codewords per CU) and there is no workgroup barrier at all.
-// The steps are those of km_fused_kernel (same screens, margins, drift bound,
-// binade scans and divisions): the real and the imaginary chains are summed
-// by the same wave one after the other.
+// One wave (and one workgroup) per codeword: the production k-means.  There
+// is no LDS copy of y: the symbols are read where they lie (HBM, then L2 /
+// Infinity Cache for the iterations' re-reads: coalesced 64-symbol words for
+// the assignment and the rebuilds); a word's membership bits and drift
+// threshold live in the registers of lane = word (S <= 4096); LDS holds the
+// cluster-0 members' VALUES in ascending symbol order (capacity S/3; a larger
+// cluster 0, seen only on degenerate inputs, is summed straight from the
+// words), the cluster points, the constellation and the launch constants
+// (6.3 KB per PEG2304/QPSK codeword).  Residency is set by registers (6 waves
+// per SIMD) and there is no workgroup barrier at all.  The real and the
+// imaginary chains are summed by the same wave one after the other (both in
+// one scan step measured slower: more registers).
 #ifndef KML_KM_WAVE_OCC
 #define KML_KM_WAVE_OCC 6  // waves per SIMD (registers <= 512 / OCC): 6 (80 VGPRs, 9 spilled) 2.75 ms, 5 3.04, 4 3.31
 #endif
@@ -1430,12 +985,9 @@ template <int KC>
 bool run_kmeans_wave(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
                      double2 *h_hat, double2 *h4, double2 *hat_out, hipStream_t s, hipError_t &err) {
   const size_t lds = (size_t)kWaveWpg * km_wave_lds(S, KC).stride;
-  if (S > 64 * kFusedMaxW || lds > 160 * 1024) return false;
-  // default: this kernel up to 16 points; 64QAM's 64-distance screens go to
-  // the two-wave kernel, which splits each codeword's words over two waves
-  // (PEG8064/64QAM, 4096 codewords: 0.64 vs 0.73 ms); KML_KMEANS=wave / fused forces
-  const char *e = getenv("KML_KMEANS");
-  if (e ? e[0] != 'w' : KC > 16) return false;
+  if (S > kMaxS || lds > 160 * 1024) return false;
+  if (const char *e = getenv("KML_KMEANS"))
+    if (e[0] == 's') return false;  // KML_KMEANS=split: the two-launch form (A/B)
   err = hipFuncSetAttribute((const void *)km_wave_kernel<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return true;
   int incremental = 1, scan = 1;
@@ -1448,32 +1000,10 @@ bool run_kmeans_wave(const double *cons, const double *rot, const double2 *y, in
 }
 
 template <int KC>
-bool run_kmeans_fused(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
-                      double2 *h_hat, double2 *h4, double2 *hat_out, hipStream_t s, hipError_t &err) {
-  const size_t lds = (size_t)km_lds(S).bytes;
-  if (S > 64 * kFusedMaxW || lds > 128 * 1024) return false;
-  if (const char *e = getenv("KML_KMEANS"))
-    if (e[0] == 's') return false;  // KML_KMEANS=split: the two-launch form (A/B)
-  err = hipFuncSetAttribute((const void *)km_fused_kernel<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (err != hipSuccess) return true;
-  int incremental = 1;  // KML_KM_INCR=0: assign every word every iteration (A/B)
-  if (const char *e = getenv("KML_KM_INCR")) incremental = e[0] != '0';
-  int scan = 1;  // KML_KM_SCAN=0: the two-lane sequential sums (A/B)
-  if (const char *e = getenv("KML_KM_SCAN")) scan = e[0] != '0';
-  int bal = 1;  // KML_KM_BAL=0: each wave assigns its own words (w % 2) instead of the flagged words by rank (A/B)
-  if (const char *e = getenv("KML_KM_BAL")) bal = e[0] != '0';
-  hipLaunchKernelGGL(km_fused_kernel<KC>, dim3(B), dim3(kFusedT), lds, s, cons, rot, y, S, iters, h_hat, h4, hat_out,
-                     incremental, scan, bal);
-  err = hipGetLastError();
-  return true;
-}
-
-template <int KC>
 hipError_t run_kmeans(const double *cons, const double *rot, const double2 *y, int S, int iters, int B,
                       KmState *st, uint64_t *mem, double2 *h_hat, double2 *h4, double2 *hat_out, hipStream_t s) {
   hipError_t ferr = hipSuccess;
   if (run_kmeans_wave<KC>(cons, rot, y, S, iters, B, h_hat, h4, hat_out, s, ferr)) return ferr;
-  if (run_kmeans_fused<KC>(cons, rot, y, S, iters, B, h_hat, h4, hat_out, s, ferr)) return ferr;
   const int Sw = (S + 63) / 64;
   const dim3 lanes((B + 63) / 64), l64(64);
   hipLaunchKernelGGL(km_init_kernel, lanes, l64, 0, s, cons, y, S, B, st);

@@ -409,7 +409,7 @@ def test_fused_demap_matches_separate(data_dir, blind, monkeypatch):
     ("PEG2304regular0.5.txt", "4bit_16QAM_phi1.txt", 8.0, 50),
     ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", 6.77, 30),
 ])
-@pytest.mark.parametrize("kernel", ["fused", "wave", "split"])
+@pytest.mark.parametrize("kernel", ["wave", "split"])
 def test_kmeans_vs_oracle(data_dir, matrix, modem, snr, n, kernel, monkeypatch):
     monkeypatch.setenv("KML_KMEANS", kernel)
     ctx = ctx_for(data_dir, matrix, modem, False)
@@ -455,26 +455,22 @@ def test_kmeans_adversarial_ties(data_dir, modem):
         assert np.array_equal(hh[b], ref, equal_nan=True), b
 
 
-@pytest.mark.parametrize("mode", ["fused", "fused_sequential_sum", "fused_owned_words", "wave", "wave_sequential_sum",
-                                  "wave_every_word", "split"])
+@pytest.mark.parametrize("mode", ["wave", "wave_sequential_sum", "wave_every_word", "split"])
 @pytest.mark.parametrize("modem", ["2bits_QPSK.txt", "4bit_16QAM_Gray.txt", "6bits_64QAM_Gray.txt"])
 def test_kmeans_cumulative_sum_adversarial(data_dir, modem, mode, monkeypatch):
     """The k-means kernels' cumulative cluster-0 sums (kmeans.hip
-    ordered_sum_wave / ordered_sum_vals2: binade-segmented grid scans, tie
+    ordered_sum_vals1: binade-segmented grid scans, tie
     parities, binade exits) and their incremental assignment against the
     oracle's sequential kmeans.cc:33-46, on inputs built to hit their corner
     cases: noise on a coarse dyadic grid (ties), a cluster-0 centre on an axis
     (sums that change sign), tiny and huge channels (extreme binades;
     thresholds past the float range), NaN / inf symbols (the complex products'
-    infinity recovery) and realistic frames; with the two-wave kernel
-    (KML_KMEANS=fused), its two-lane sequential sums (KML_KM_SCAN=0) and each
-    wave assigning its own words (KML_KM_BAL=0), the one-wave kernel
+    infinity recovery) and realistic frames; with the one-wave kernel
     (KML_KMEANS=wave: the members' values in LDS) with and without its scans
     and with every word re-assigned every iteration (KML_KM_INCR=0), and the
     two-launch form (KML_KMEANS=split, the path of S > 4096)."""
     monkeypatch.setenv("KML_KMEANS", mode.split("_")[0])
     monkeypatch.setenv("KML_KM_SCAN", "0" if mode.endswith("sequential_sum") else "1")
-    monkeypatch.setenv("KML_KM_BAL", "0" if mode.endswith("owned_words") else "1")
     monkeypatch.setenv("KML_KM_INCR", "0" if mode.endswith("every_word") else "1")
     matrix = "PEG8064regular0.5.txt" if "64QAM" in modem else "PEG2304regular0.5.txt"
     ctx = ctx_for(data_dir, matrix, modem, False)

@@ -1,4 +1,4 @@
-"""CPU checks of the algorithms behind the fused k-means kernel's shortcuts
+"""CPU checks of the algorithms behind the k-means kernel's shortcuts
 (kmeans.hip): the binade-segmented scan that replaces the sequential
 cluster-0 sum must equal the left-to-right fp64 sum bit for bit, including
 signed zeros, ties, binade and sign changes, huge/tiny/non-finite values."""

@@ -1,4 +1,4 @@
-"""Phase timing of the fused k-means kernel (kmeans.hip, km_fused_kernel) from
+"""Phase timing of the k-means kernel (kmeans.hip, km_wave_kernel) from
 its s_memtime stamps.  Needs the stamps build:
 
     make stamps
