@@ -5,7 +5,7 @@ ones, iteration budgets 20, 1 and 0) with fresh priors, and stops at the first
 abort, printing the site the library reports (group barrier / v2c / c2v mailbox
 poll / early-stop flag poll) and the workgroup.
 
-    python tools/stress_part.py [rounds]
+    python tools/stress_part.py [rounds] [tagged (1) | barrier exchange only (0)]
 """
 import gzip
 import os
@@ -22,12 +22,13 @@ import kmldpc_amd as K  # noqa: E402
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+    tagged = sys.argv[2] if len(sys.argv) > 2 else "1"
     d = tempfile.mkdtemp(prefix="kml_stress_")
     src = os.path.join(REPO, "tests", "golden", "data")
     for fn in ("PEG8064regular0.5.txt.gz", "6bits_64QAM_Gray.txt.gz"):
         with gzip.open(os.path.join(src, fn), "rb") as g, open(os.path.join(d, fn[:-3]), "wb") as f:
             f.write(g.read())
-    os.environ["KML_PART_TAGGED"] = "1"
+    os.environ["KML_PART_TAGGED"] = tagged
     ctx = K.Context(matrix_file=os.path.join(d, "PEG8064regular0.5.txt"),
                     modem_file=os.path.join(d, "6bits_64QAM_Gray.txt"), max_iter=20, device=0)
     assert ctx.dims["part_group"] == 4
