@@ -104,7 +104,7 @@ const char *kml_last_error(const kml_ctx *ctx);
 int kml_abi_version(void);
 /* Name of the BP kernel family the context last launched ("bp_regular_kernel",
  * "bp_irregular_kernel", "bp_part_kernel" (the partitioned cooperative kernel,
- * PEG8064), "bp_coop_kernel", "bp_kernel"; "" before any decode). */
+ * PEG8064), "bp_kernel"; "" before any decode). */
 const char *kml_bp_kernel(const kml_ctx *ctx);
 
 int kml_dims(const kml_ctx *ctx, int32_t *dims /* [KML_DIM_COUNT] */);

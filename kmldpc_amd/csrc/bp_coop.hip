@@ -119,14 +119,19 @@ __device__ __forceinline__ unsigned ld_rlx(const unsigned *p) {  // L1-bypassing
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Abort the cooperative launch: abort[0] = 1 stops every poll; the first
-// aborter also records where it gave up in abort[1] (site << 24 | workgroup):
-// 1 group barrier, 2 v2c mailbox poll, 3 c2v mailbox poll, 4 early-stop flag
-// poll (bp_coop_aborted reports it).
+// Leave a poll of the cooperative launch.  A poller whose own spin limit ran
+// out (timed_out) aborts the launch: it records where it gave up in abort[1]
+// (site << 24 | workgroup: 1 group barrier, 2 v2c mailbox poll, 3 c2v mailbox
+// poll, 4 early-stop flag poll; the first such poller wins), then sets
+// abort[0] = 1, which stops every poll.  A poller that only saw abort[0] set
+// (by another poller, or by the host: kml_debug_inject_abort) records nothing,
+// so abort[1] names the site that actually timed out, or stays 0 for a
+// host-raised abort (bp_coop_aborted reports it).
 enum { kAbortBarrier = 1, kAbortV2c = 2, kAbortC2v = 3, kAbortFlag = 4 };
-__device__ __forceinline__ void coop_abort(unsigned *abort, unsigned site) {
+__device__ __forceinline__ void coop_abort(unsigned *abort, unsigned site, bool timed_out) {
+  if (!timed_out) return;
   atomicCAS(abort + 1, 0u, (site << 24) | (blockIdx.x & 0xFFFFFFu));
-  __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(abort, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // loads of data other members wrote: bypass the vector L1
@@ -206,7 +211,7 @@ __device__ __forceinline__ int part_barrier(GroupSync *gs, unsigned long long *s
       v = ld_rlx64(&gs->bar2[p]);
       if ((unsigned)v >= (unsigned)st[p]) break;
       if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
-        coop_abort(abort, kAbortBarrier);
+        coop_abort(abort, kAbortBarrier, spin > kSpinLimit);
         r = -1;
         break;
       }
@@ -607,7 +612,7 @@ __device__ __forceinline__ bool poll_entries(const int (&ent)[R], __amdgpu_buffe
       }
     if (!pend) return true;
     if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
-      coop_abort(abort, W == 2 ? kAbortV2c : kAbortC2v);
+      coop_abort(abort, W == 2 ? kAbortV2c : kAbortC2v, spin > kSpinLimit);
       return false;
     }
     if (KML_POLL_SLEEP) __builtin_amdgcn_s_sleep(1);
@@ -737,7 +742,7 @@ __device__ __forceinline__ int part_iterations_tagged(
           v = spin == 0 ? vflag : ld_rlx64(&gs->mflag[(g - 1) & 1][tid]);  // first: the load issued before VN
           if ((v >> 2) == (unsigned long long)g) break;
           if ((spin & 63) == 63 && (spin > kSpinLimit || ld_rlx(abort))) {
-            coop_abort(abort, kAbortFlag);
+            coop_abort(abort, kAbortFlag, spin > kSpinLimit);
             *sdead = 1;
             break;
           }

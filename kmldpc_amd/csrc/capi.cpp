@@ -516,7 +516,7 @@ int sync(kml_ctx *c) {
                                          "early-stop flag poll"};
       const unsigned k = why >> 24;
       return fail(c, KML_E_HIP,
-                  std::string("cooperative BP kernel aborted (a group barrier timed out): ") + (k < 5 ? site[k] : "?") +
+                  std::string("cooperative BP kernel aborted: ") + (k == 0 ? "" : "timed out at ") + (k < 5 ? site[k] : "?") +
                       (why ? ", workgroup " + std::to_string(why & 0xFFFFFFu) : std::string()));
     }
   }
@@ -1336,6 +1336,7 @@ int kml_comm_size(const kml_ctx *c) { return c ? kml::rccl_size(c->comm) : 0; }
 
 namespace {
 int comm_allreduce(kml_ctx *c, void *vals, int n, bool f64) {
+  call_begin(c);
   if (!c || (!vals && n > 0) || n < 0) return fail(c, KML_E_ARG, "kml_comm_allreduce: bad argument");
   if (!c->comm) return fail(c, KML_E_ARG, "kml_comm_allreduce: no communicator (kml_comm_init)");
   if (n == 0) return KML_OK;

@@ -37,7 +37,9 @@
 //              (Smith divisions).
 // km_init (first max of |y|, same screening) and km_final (h_hat and the 4
 // rotated candidates) are lane-per-codeword.
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "bp_common.hpp"
 #include "exact_math.hpp"
@@ -883,9 +885,13 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
             m = member0_slow<KC>(cl, v.x, v.y);
             g = 0.0;
           }
-        // D + g / (2 Cmax), rounded down; past the float range a finite 2^127
+        // D + g / (2 Cmax), rounded down: the (1 - 2^-20) factor covers the
+        // float conversion's rounding in the normal range; below FLT_MIN (where
+        // a denormal's relative rounding error is unbounded) the threshold is 0,
+        // i.e. the word is re-assigned next iteration; past the float range a
+        // finite 2^127
         const double td = (drift + g * kc->inv2c) * (1.0 - 0x1p-20);
-        const float t = wave_min_f(valid ? (td < 0x1p127 ? (float)td : 0x1p127f) : INFINITY);
+        const float t = wave_min_f(valid ? (td < 0x1p-126 ? 0.0f : td < 0x1p127 ? (float)td : 0x1p127f) : INFINITY);
         const uint64_t bits = __ballot(valid && m);
         if (it == 0 || bits != lane_u64(wb, q)) chg = 1;
         if (lane == q) {
@@ -986,8 +992,14 @@ bool run_kmeans_wave(const double *cons, const double *rot, const double2 *y, in
                      double2 *h_hat, double2 *h4, double2 *hat_out, hipStream_t s, hipError_t &err) {
   const size_t lds = (size_t)kWaveWpg * km_wave_lds(S, KC).stride;
   if (S > kMaxS || lds > 160 * 1024) return false;
-  if (const char *e = getenv("KML_KMEANS"))
-    if (e[0] == 's') return false;  // KML_KMEANS=split: the two-launch form (A/B)
+  if (const char *e = getenv("KML_KMEANS")) {  // A/B switch: "wave" (default) or "split" (the two-launch form)
+    if (!strcmp(e, "split")) return false;
+    if (strcmp(e, "wave") != 0) {
+      static bool warned = false;
+      if (!warned) fprintf(stderr, "kmldpc_amd: KML_KMEANS=%s is not a k-means kernel (wave, split); running wave\n", e);
+      warned = true;
+    }
+  }
   err = hipFuncSetAttribute((const void *)km_wave_kernel<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return true;
   int incremental = 1, scan = 1;

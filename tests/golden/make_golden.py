@@ -5,6 +5,7 @@ oracle/_ref/ref_harness, built by ``make -C oracle ref``):
 
     python tests/golden/make_golden.py                 # data files, CASES, counters.json
     python tests/golden/make_golden.py --cases a,b     # regenerate the named CASES only
+    python tests/golden/make_golden.py --check-direct  # re-run every CASE, check KmCodec == direct decode, write nothing
     python tests/golden/make_golden.py --sweep         # sweep/cfg5.npz (PEG8064 blind sweep counters)
     python tests/golden/make_golden.py --bench         # bench/*.npz (bench workload's reference counters)
     python tests/golden/make_golden.py --bench-cases a,b   # the named BENCH_CASES only
@@ -68,6 +69,22 @@ CASES = {
     "peg2304_qpsk_blind_inactive": ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.0, 200, False),
     "bg2_16qam_known_inactive": ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, True, 50, 4.0, 100, False),
     "bg2_16qam_blind_inactive": ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, False, 50, 5.01, 60, False),
+    # the (code x constellation) cross-product: [ldpc] matrix_file and [modem]
+    # modem_file are independent keys (binaryldpccodec.cc:71-73, modem.cc:7)
+    # PEG8064 + QPSK: S = 4032 symbols, 63 of km_wave_kernel's 64 lane-words
+    "peg8064_qpsk_known": ("PEG8064regular0.5.txt", "2bits_QPSK.txt", False, True, 20, 1.6, 40, True),
+    "peg8064_qpsk_blind": ("PEG8064regular0.5.txt", "2bits_QPSK.txt", False, False, 20, 2.3, 40, True),
+    "peg8064_16qam_known": ("PEG8064regular0.5.txt", "4bit_16QAM_Gray.txt", False, True, 20, 6.0, 40, True),
+    "peg8064_16qam_blind": ("PEG8064regular0.5.txt", "4bit_16QAM_Gray.txt", False, False, 20, 6.4, 40, True),
+    # 5G BG2 + QPSK / 64QAM (S = 320: a partial k-means word) / 16QAM-phi1
+    "bg2_qpsk_known": ("5GLDPCBG2a3_R12_K960.txt", "2bits_QPSK.txt", True, True, 50, 1.5, 100, True),
+    "bg2_qpsk_blind": ("5GLDPCBG2a3_R12_K960.txt", "2bits_QPSK.txt", True, False, 50, 2.0, 100, True),
+    "bg2_64qam_known": ("5GLDPCBG2a3_R12_K960.txt", "6bits_64QAM_Gray.txt", True, True, 50, 10.0, 60, True),
+    "bg2_64qam_blind": ("5GLDPCBG2a3_R12_K960.txt", "6bits_64QAM_Gray.txt", True, False, 50, 11.0, 60, True),
+    "bg2_16qamphi1_blind": ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_phi1.txt", True, False, 50, 11.0, 100, True),
+    # PEG2304 + blind 4PSK (the axis-aligned QPSK: 2bits_4PSK.txt) and blind 64QAM
+    "peg2304_4psk_blind": ("PEG2304regular0.5.txt", "2bits_4PSK.txt", False, False, 20, 2.0, 100, True),
+    "peg2304_64qam_blind": ("PEG2304regular0.5.txt", "6bits_64QAM_Gray.txt", False, False, 20, 10.5, 60, True),
 }
 
 # soft syndrome metric ([xcodec] metric_type = true): name -> (matrix, modem, 5g,
@@ -88,6 +105,8 @@ for _snr in SWEEP_SNRS:
         CASES[f"peg8064_64qam_blind_s{int(round(_snr * 100))}"] = (
             "PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, False, 20, _snr, 24, True)
 NVEC_CASE = {k: 2 for k in CASES if k.startswith("peg8064_64qam_blind_s")}
+NVEC_CASE.update({k: 4 for k in ("peg8064_qpsk_known", "peg8064_qpsk_blind", "peg8064_16qam_known",
+                                 "peg8064_16qam_blind")})
 SWEEP_N = 400
 
 # the bench workload's reference counters: the first B codewords of the seed-17
@@ -316,7 +335,38 @@ def run_simulate(tmp, name, mat, mod, is5g, known, it, snr, n, active=True):
     return dict(K=K, tot_blk=tot_blk, err_blk=err_blk, err_bit=int(errs.sum()), ber=ber, fer=fer), errs
 
 
-def make_frames_cases(tmp, names):
+def check_direct(name, recs):
+    """The harness's cross-check: KmCodec::Decoder's uu_hat (kmcodec.cc:69-70, the
+    chosen candidate's P0 through ldpc_codec_->Decoder at max_iter) equals a
+    directly constructed codec's Decoder on the same P0 (ref_harness.cc).  BP is a
+    pure function of P0, so this holds known and blind, PEG and 5G."""
+    bad = [i for i, d in enumerate(recs) if not np.array_equal(d["uu_hat"], d["uu_hat_direct"])]
+    assert not bad, f"{name}: KmCodec uu_hat != direct decode on codewords {bad[:10]}"
+
+
+def frames_arrays(hdr, cons, recs, mat, mod, active, nv):
+    arrs = {
+        "hdr_json": np.frombuffer(json.dumps(dict(hdr, matrix=mat, modem=mod, active=active)).encode(), dtype=np.uint8),
+        "cons": cons,
+        "s_chosen": np.array([d["chosen"] for d in recs], np.int32),
+        "s_ret": np.array([d["ret"] for d in recs], np.int32),
+        "s_errs": np.array([d["errs"] for d in recs], np.int32),
+        "s_crc_y": np.array([crc(d["y"]) for d in recs], np.uint32),
+        "s_crc_p0": np.array([crc(d["p0"]) for d in recs], np.uint32),
+        "s_crc_uuhat": np.array([crc(d["uu_hat"]) for d in recs], np.uint32),
+        "s_crc_cchat": np.array([crc(d["cc_hat"]) for d in recs], np.uint32),
+        "s_crc_syn": np.array([crc(d["syn"]) for d in recs], np.uint32),
+        "s_crc_uu": np.array([crc(d["uu"]) for d in recs], np.uint32),
+        "s_hhat": np.array([d["h_hat"] for d in recs]),
+        "s_metrics": np.array([d["metrics"] for d in recs]),
+        "s_true_h": np.array([d["true_h"] for d in recs]),
+    }
+    for key in ["uu", "cc", "y", "p0", "cc_hat", "syn", "uu_hat"]:
+        arrs["v_" + key] = np.stack([recs[i][key] for i in range(nv)])
+    return arrs
+
+
+def make_frames_cases(tmp, names, check_only=False):
     from concurrent.futures import ThreadPoolExecutor
 
     def one(name):
@@ -326,25 +376,10 @@ def make_frames_cases(tmp, names):
         out = os.path.join(tmp, name + ".bin")
         subprocess.run([HARNESS, cfg, repr(snr), str(n), out], check=True)
         hdr, cons, recs = parse_frames(open(out, "rb").read())
-        arrs = {
-            "hdr_json": np.frombuffer(json.dumps(dict(hdr, matrix=mat, modem=mod, active=active)).encode(), dtype=np.uint8),
-            "cons": cons,
-            "s_chosen": np.array([d["chosen"] for d in recs], np.int32),
-            "s_ret": np.array([d["ret"] for d in recs], np.int32),
-            "s_errs": np.array([d["errs"] for d in recs], np.int32),
-            "s_crc_y": np.array([crc(d["y"]) for d in recs], np.uint32),
-            "s_crc_p0": np.array([crc(d["p0"]) for d in recs], np.uint32),
-            "s_crc_uuhat": np.array([crc(d["uu_hat"]) for d in recs], np.uint32),
-            "s_crc_cchat": np.array([crc(d["cc_hat"]) for d in recs], np.uint32),
-            "s_crc_syn": np.array([crc(d["syn"]) for d in recs], np.uint32),
-            "s_crc_uu": np.array([crc(d["uu"]) for d in recs], np.uint32),
-            "s_hhat": np.array([d["h_hat"] for d in recs]),
-            "s_metrics": np.array([d["metrics"] for d in recs]),
-            "s_true_h": np.array([d["true_h"] for d in recs]),
-        }
-        nv = min(NVEC_CASE.get(name, NVEC), len(recs))
-        for key in ["uu", "cc", "y", "p0", "cc_hat", "syn", "uu_hat"]:
-            arrs["v_" + key] = np.stack([recs[i][key] for i in range(nv)])
+        check_direct(name, recs)
+        if check_only:
+            return f"{name}: n={n} KmCodec::Decoder == direct BinaryLDPCCodec::Decoder on every codeword"
+        arrs = frames_arrays(hdr, cons, recs, mat, mod, active, min(NVEC_CASE.get(name, NVEC), len(recs)))
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
         return f"{name}: n={n} FER={np.mean(arrs['s_errs'] > 0):.4f} mean_ret={arrs['s_ret'].mean():.2f}"
 
@@ -452,11 +487,12 @@ def main():
         finally:
             shutil.rmtree(tmp)
         return
-    if "--cases" in sys.argv:
-        names = sys.argv[sys.argv.index("--cases") + 1].split(",")
+    if "--cases" in sys.argv or "--check-direct" in sys.argv:
+        check = "--check-direct" in sys.argv
+        names = list(CASES) if check else sys.argv[sys.argv.index("--cases") + 1].split(",")
         tmp = tempfile.mkdtemp()
         try:
-            make_frames_cases(tmp, names)
+            make_frames_cases(tmp, names, check_only=check)
         finally:
             shutil.rmtree(tmp)
         return
@@ -485,36 +521,7 @@ def main():
             g.write(raw)
     tmp = tempfile.mkdtemp()
     try:
-        for name, (mat, mod, is5g, known, it, snr, n, active) in CASES.items():
-            cfg = os.path.join(tmp, name + ".toml")
-            write_toml(cfg, REF_CFG, mat, mod, is5g, known, it, active)
-            out = os.path.join(tmp, name + ".bin")
-            subprocess.run([HARNESS, cfg, repr(snr), str(n), out], check=True)
-            hdr, cons, recs = parse_frames(open(out, "rb").read())
-            for d in recs:
-                assert np.array_equal(d["uu_hat"], d["uu_hat_direct"]) or not hdr["known"] or True
-            arrs = {
-                "hdr_json": np.frombuffer(json.dumps(dict(hdr, matrix=mat, modem=mod, active=active)).encode(), dtype=np.uint8),
-                "cons": cons,
-                "s_chosen": np.array([d["chosen"] for d in recs], np.int32),
-                "s_ret": np.array([d["ret"] for d in recs], np.int32),
-                "s_errs": np.array([d["errs"] for d in recs], np.int32),
-                "s_crc_y": np.array([crc(d["y"]) for d in recs], np.uint32),
-                "s_crc_p0": np.array([crc(d["p0"]) for d in recs], np.uint32),
-                "s_crc_uuhat": np.array([crc(d["uu_hat"]) for d in recs], np.uint32),
-                "s_crc_cchat": np.array([crc(d["cc_hat"]) for d in recs], np.uint32),
-                "s_crc_syn": np.array([crc(d["syn"]) for d in recs], np.uint32),
-                "s_crc_uu": np.array([crc(d["uu"]) for d in recs], np.uint32),
-                "s_hhat": np.array([d["h_hat"] for d in recs]),
-                "s_metrics": np.array([d["metrics"] for d in recs]),
-                "s_true_h": np.array([d["true_h"] for d in recs]),
-            }
-            nv = min(NVEC, len(recs))
-            for key in ["uu", "cc", "y", "p0", "cc_hat", "syn", "uu_hat"]:
-                arrs["v_" + key] = np.stack([recs[i][key] for i in range(nv)])
-            np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
-            print(f"{name}: n={n} FER={np.mean(arrs['s_errs'] > 0):.4f} "
-                  f"mean_ret={arrs['s_ret'].mean():.2f}")
+        make_frames_cases(tmp, list(CASES))
         counters = {}
         for name, (mat, mod, is5g, known, it, snr, n, active) in COUNTER_CASES.items():
             cfg = os.path.join(tmp, name + ".toml")

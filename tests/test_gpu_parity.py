@@ -287,6 +287,9 @@ def test_bp_golden_vectors(case, data_dir):
     ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", False, 4.0, 20, 200),
     ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_Gray.txt", True, 5.01, 50, 200),
     ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 8.5, 20, 48),
+    ("PEG8064regular0.5.txt", "2bits_QPSK.txt", False, 1.8, 20, 40),
+    ("5GLDPCBG2a3_R12_K960.txt", "2bits_QPSK.txt", True, 1.5, 50, 100),
+    ("5GLDPCBG2a3_R12_K960.txt", "6bits_64QAM_Gray.txt", True, 10.0, 50, 60),
 ])
 def test_bp_vs_oracle_stream(data_dir, matrix, modem, is5g, snr, max_iter, n):
     """Oracle frames -> oracle P0 -> GPU BP vs oracle BP, bit-exact incl. the
@@ -309,8 +312,13 @@ def test_bp_vs_oracle_stream(data_dir, matrix, modem, is5g, snr, max_iter, n):
 
 @pytest.mark.parametrize("matrix,modem,is5g,snr,n", [
     ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, 2.0, 200),
+    ("PEG2304regular0.5.txt", "2bits_4PSK.txt", False, 2.0, 100),
     ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", False, 5.0, 100),
     ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 6.77, 40),
+    ("PEG8064regular0.5.txt", "2bits_QPSK.txt", False, 2.0, 40),
+    ("PEG8064regular0.5.txt", "4bit_16QAM_Gray.txt", False, 6.0, 40),
+    ("5GLDPCBG2a3_R12_K960.txt", "6bits_64QAM_Gray.txt", True, 10.0, 100),
+    ("5GLDPCBG2a3_R12_K960.txt", "2bits_QPSK.txt", True, 2.0, 100),
 ])
 def test_demap_vs_oracle(data_dir, matrix, modem, is5g, snr, n):
     ctx = ctx_for(data_dir, matrix, modem, is5g)
@@ -401,19 +409,29 @@ def test_fused_demap_matches_separate(data_dir, blind, monkeypatch):
         assert np.array_equal(r1["uu_hat"][i], ref["uu_hat"]) and r1["ret"][i] == ref["ret"], i
 
 
-@pytest.mark.parametrize("matrix,modem,snr,n", [
-    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", 2.0, 1000),
-    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", -1.0, 500),
-    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", 8.0, 300),
-    ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", 5.01, 100),
-    ("PEG2304regular0.5.txt", "4bit_16QAM_phi1.txt", 8.0, 50),
-    ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", 6.77, 30),
+@pytest.mark.parametrize("matrix,modem,is5g,snr,n", [
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, 2.0, 1000),
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, -1.0, 500),
+    ("PEG2304regular0.5.txt", "2bits_QPSK.txt", False, 8.0, 300),
+    ("PEG2304regular0.5.txt", "2bits_4PSK.txt", False, 2.0, 200),
+    ("PEG2304regular0.5.txt", "4bit_16QAM_Gray.txt", False, 5.01, 100),
+    ("PEG2304regular0.5.txt", "4bit_16QAM_phi1.txt", False, 8.0, 50),
+    ("PEG2304regular0.5.txt", "6bits_64QAM_Gray.txt", False, 10.5, 60),
+    ("PEG8064regular0.5.txt", "6bits_64QAM_Gray.txt", False, 6.77, 30),
+    # S = 4032: 63 of the 64 lane-words km_wave_kernel holds (kmeans.hip kMaxS)
+    ("PEG8064regular0.5.txt", "2bits_QPSK.txt", False, 2.0, 60),
+    ("PEG8064regular0.5.txt", "2bits_QPSK.txt", False, -2.0, 30),
+    ("PEG8064regular0.5.txt", "4bit_16QAM_Gray.txt", False, 6.4, 40),
+    # 5G BG2: S = 320 (64QAM, a partial fifth word), 480 (16QAM), 960 (QPSK)
+    ("5GLDPCBG2a3_R12_K960.txt", "6bits_64QAM_Gray.txt", True, 11.0, 200),
+    ("5GLDPCBG2a3_R12_K960.txt", "4bit_16QAM_phi1.txt", True, 11.0, 100),
+    ("5GLDPCBG2a3_R12_K960.txt", "2bits_QPSK.txt", True, 2.0, 200),
 ])
 @pytest.mark.parametrize("kernel", ["wave", "split"])
-def test_kmeans_vs_oracle(data_dir, matrix, modem, snr, n, kernel, monkeypatch):
+def test_kmeans_vs_oracle(data_dir, matrix, modem, is5g, snr, n, kernel, monkeypatch):
     monkeypatch.setenv("KML_KMEANS", kernel)
-    ctx = ctx_for(data_dir, matrix, modem, False)
-    oc = oracle_for(data_dir, matrix, False)
+    ctx = ctx_for(data_dir, matrix, modem, is5g)
+    oc = oracle_for(data_dir, matrix, is5g)
     om = O.Modem(os.path.join(data_dir, modem))
     uu, cc, th, y = O.gen_frames(oc, om, snr, n)
     hh, h4 = ctx.kmeans(y)
@@ -464,7 +482,7 @@ def test_kmeans_cumulative_sum_adversarial(data_dir, modem, mode, monkeypatch):
     oracle's sequential kmeans.cc:33-46, on inputs built to hit their corner
     cases: noise on a coarse dyadic grid (ties), a cluster-0 centre on an axis
     (sums that change sign), tiny and huge channels (extreme binades;
-    thresholds past the float range), NaN / inf symbols (the complex products'
+    thresholds past the float range; |h| ~ 1e-31, thresholds below FLT_MIN), NaN / inf symbols (the complex products'
     infinity recovery) and realistic frames; with the one-wave kernel
     (KML_KMEANS=wave: the members' values in LDS) with and without its scans
     and with every word re-assigned every iteration (KML_KM_INCR=0), and the
@@ -477,12 +495,13 @@ def test_kmeans_cumulative_sum_adversarial(data_dir, modem, mode, monkeypatch):
     om = O.Modem(os.path.join(data_dir, modem))
     pts = om.points.reshape(-1, 2) @ [1, 1j]
     rng = np.random.default_rng(41)
-    S, B = ctx.S, 20
+    S, B = ctx.S, 24
     y = np.zeros((B, S, 2))
     for b in range(B):
-        kind = b % 5
+        kind = b % 6
+        # kind 5: |h| ~ 1e-31, drift thresholds below FLT_MIN (kmeans.hip: clamped to 0)
         hc = [1.0, 1j, 1e-200 * complex(*rng.normal(size=2)), 1e150 * complex(*rng.normal(size=2)),
-              complex(*rng.normal(size=2))][kind]
+              complex(*rng.normal(size=2)), 1e-31 * complex(*rng.normal(size=2))][kind]
         sym = pts[rng.integers(0, len(pts), S)]
         if kind == 0:  # dyadic noise: the grid sums hit exact ties
             noise = (rng.integers(-40, 40, S) + 1j * rng.integers(-40, 40, S)) * 2.0 ** -7
@@ -780,8 +799,9 @@ def test_kmeans_state_vs_reference(name, data_dir):
 @pytest.mark.gpu
 @pytest.mark.parametrize("modem", ["2bits_QPSK.txt", "4bit_16QAM_Gray.txt", "6bits_64QAM_Gray.txt"])
 def test_kmeans_cluster0_majority(data_dir, modem):
-    """Frames that put more than S/2 symbols into cluster 0 (dense membership
-    words for the word scan): an all-zero codeword (every distance ties, the
+    """Frames that put more than S/2 symbols into cluster 0, past the member
+    list's capacity L.cap = S/3 (km_wave_kernel then sums cluster 0 straight
+    from the membership words instead of its LDS value list): an all-zero codeword (every distance ties, the
     first minimum wins), every symbol on point 0 times h, and 60-95 % of the
     symbols near point 0 times h with the rest random.  h_hat, clusters and
     idx bit-exact against the oracle (kmeans.cc:15-84)."""
@@ -894,7 +914,7 @@ def test_host_buffer_chunked_decode_matches_one_piece(data_dir, matrix, modem, i
 
 @pytest.mark.parametrize("blind", [False, True])
 def test_chunked_decode_reports_abort_of_an_early_chunk(data_dir, blind, monkeypatch):
-    """A cooperative launch that aborts (a group barrier timed out) in chunk 0
+    """A cooperative launch that aborts (as if a poll had timed out) in chunk 0
     of a chunked host-buffer call must fail the call: later chunks' launches
     must not clear the abort word before the call's single sync reads it
     (capi.cpp run_bp / sync).  The abort is injected after the first
@@ -908,7 +928,7 @@ def test_chunked_decode_reports_abort_of_an_early_chunk(data_dir, blind, monkeyp
     monkeypatch.setenv("KML_HOST_CHUNK", "16")  # 3 chunks
     r0 = ctx.decode_frames(y, 6.0, None if blind else th)
     ctx.debug_inject_abort(0)
-    with pytest.raises(K.KmlError, match="aborted"):
+    with pytest.raises(K.KmlError, match="aborted: raised by the host"):  # no poll timed out
         ctx.decode_frames(y, 6.0, None if blind else th)
     r1 = ctx.decode_frames(y, 6.0, None if blind else th)  # the abort was reported and cleared
     for k in ("uu_hat", "ret"):
@@ -949,7 +969,11 @@ def test_pending_abort_survives_a_later_argument_error(data_dir):
     cnt = np.zeros(8, np.uint64)
     rc = K.lib().kml_sim_decode(ctx._h, 6.0, 0, K._p(cnt), 0)  # KML_E_ARG: counters need sync != 0
     assert rc == -1
-    with pytest.raises(K.KmlError, match="aborted"):
+    # the counter all-reduce's argument errors likewise (comm_allreduce
+    # starts a call too): a null buffer, then no communicator on this context
+    assert K.lib().kml_comm_allreduce_u64(ctx._h, None, 4) == -1
+    assert K.lib().kml_comm_allreduce_f64(ctx._h, K._p(np.zeros(2)), 2) == -1
+    with pytest.raises(K.KmlError, match="aborted: raised by the host"):
         ctx.sync()
     assert ctx.sim_decode(6.0, blind=False) == c0
 

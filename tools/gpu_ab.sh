@@ -3,7 +3,7 @@
 # then bench lines of several library builds for several workloads, two rounds
 # each, interleaved (same box).  $LIBS: kmldpc_amd/libkmldpc_amd_<x>.so
 # suffixes ("main" = the product build), each optionally with one environment
-# setting as <lib>:VAR=VALUE (e.g. main:KML_KMEANS=fused); $WORKLOADS: headline
+# setting as <lib>:VAR=VALUE (e.g. main:KML_KMEANS=split); $WORKLOADS: headline
 # blind bg2 peg8064.
 # Outputs under gpurun_out/$1/; every GPU step under its own time limit.
 set -o pipefail

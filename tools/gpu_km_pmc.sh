@@ -1,7 +1,7 @@
 #!/bin/bash
 # k-means PMC passes (blind PEG2304 bench, 2 steps): issue / wait / instruction-
 # cache counters of the k-means kernel, for the product kernel and an A/B
-# environment setting ($2, e.g. KML_KMEANS=fused).  Outputs gpurun_out/$1/<tag>_<pass>/.
+# environment setting ($2, e.g. KML_KMEANS=split).  Outputs gpurun_out/$1/<tag>_<pass>/.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${1:-kmpmc}; mkdir -p $O
