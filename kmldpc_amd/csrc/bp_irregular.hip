@@ -54,11 +54,89 @@ __device__ __forceinline__ double with_sign(double x, int bit) {
 }
 __device__ __forceinline__ int swap_pair_i(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }
 
+// Beta chains ahead (R <= KML_IRR_VN_BETA_EARLY_R): a column's backward
+// states beta_k (binaryldpccodec.cc:199-213: beta_{D-1} = (1, 1), beta_{k-1} =
+// normalise(beta_k * c2v_k)) depend on the c2v messages only, not on the
+// forward alphas, so the two chains run interleaved step by step and the
+// outputs normalise(alpha_k * beta_k) follow, independent of each other: the
+// column's dependent chain is max(D - 1, D - 1) + 1 normalisations instead of
+// (D - 1) + (D - 1) + 1.  The same operations on the same values (bit-exact),
+// in another order; the betas are held (2 D more registers).  A wave holding
+// the heaviest columns alone at the end of the VN phase runs latency-bound
+// (profiles/r05_v4_irr_stamps.txt: waves 0-2, degree 9).
+#ifndef KML_IRR_VN_BETA_EARLY_R
+#define KML_IRR_VN_BETA_EARLY_R 1
+#endif
+template <int D, int R, bool FAST>
+__device__ __forceinline__ void vn_cols_beta_early(double2 *slots, const unsigned short *const (&cs)[R],
+                                                   const double (&p)[R], unsigned char *const (&hard)[R], bool &sus) {
+  double c0s[R][D];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int k = 0; k < D; ++k) c0s[r][k] = slots[cs[r][k]].x;
+  double a0[R], a1[R], al0[R][D], al1[R][D], be0[R][D], be1[R][D];
+  int hb[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    a0[r] = p[r];
+    a1[r] = 1.0 - p[r];
+    be0[r][D - 1] = be1[r][D - 1] = 1.0;
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      // forward step k
+      al0[r][k] = a0[r];
+      al1[r][k] = a1[r];
+      const double n0 = a0[r] * c0s[r][k];
+      const double n1 = a1[r] * (1.0 - c0s[r][k]);
+      if (k + 1 < D)
+        div2<FAST>(n0, n1, n0 + n1, a0[r], a1[r], sus);
+      else
+        *hard[r] = (unsigned char)(hb[r] = hard_decision<FAST>(n0, n1, sus));
+      // backward state j - 1 from state j and c2v_j, j = D - 1 - k
+      const int j = D - 1 - k;
+      if (j > 0) {
+        const double c0 = c0s[r][j];
+        const double b0 = be0[r][j], b1 = be1[r][j];
+        if (FAST && j == D - 1) {  // beta = (1, 1): (c0, 1 - c0), its sum rounds to exactly 1 (bp_common.hpp)
+          be0[r][j - 1] = c0;
+          be1[r][j - 1] = 1.0 - c0;
+        } else {
+          div2<FAST>(b0 * c0, b1 * (1.0 - c0), b0 * c0 + b1 * (1.0 - c0), be0[r][j - 1], be1[r][j - 1], sus);
+        }
+      }
+    }
+#pragma unroll
+  for (int k = D - 1; k >= 0; --k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool unit = FAST && k == D - 1;  // beta = (1, 1)
+      const double t0 = unit ? al0[r][k] : al0[r][k] * be0[r][k];
+      const double t1 = unit ? al1[r][k] : al1[r][k] * be1[r][k];
+      double q0, q1;
+      if (unit && D == 1) {  // the prior itself (vn_cols below)
+        q0 = t0;
+        q1 = t1;
+      } else if (unit)
+        div2<FAST, true>(t0, t1, t0 + t1, q0, q1, sus);
+      else
+        div2<FAST>(t0, t1, t0 + t1, q0, q1, sus);
+      slots[cs[r][k]] = make_double2(q0, with_sign(q1, hb[r]));
+    }
+}
+
 // R columns of degree D (binaryldpccodec.cc:177-213), their chains
 // interleaved step by step so the dependent fma / rcp sequences overlap.
 template <int D, int R, bool FAST>
 __device__ __forceinline__ void vn_cols(double2 *slots, const unsigned short *const (&cs)[R], const double (&p)[R],
                                         unsigned char *const (&hard)[R], bool &sus) {
+  if constexpr (R <= KML_IRR_VN_BETA_EARLY_R && D > 2) {
+    vn_cols_beta_early<D, R, FAST>(slots, cs, p, hard, sus);
+    return;
+  }
   double c0s[R][D];
 #pragma unroll
   for (int r = 0; r < R; ++r)

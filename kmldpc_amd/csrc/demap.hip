@@ -53,7 +53,7 @@ namespace {
 #ifndef KML_DEMAP16_WAVES
 #define KML_DEMAP16_WAVES 4
 #endif
-template <int MB, bool EXACT>
+template <int MB, bool EXACT, bool ROT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? KML_DEMAP64_WAVES : MB == 4 ? KML_DEMAP16_WAVES : 1))) void demap_kernel(const double *__restrict__ cons, const double2 *__restrict__ y,
                                                     int S, int reps, const double2 *__restrict__ h, int h_stride,
                                                     const int32_t *__restrict__ h_sel, double var, int B,
@@ -63,6 +63,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? K
   // plain table otherwise (demap_common.hpp stage_exp_table_banked)
   constexpr int ES = (MB >= 6 && KML_EXPTAB_BANKED) ? kExpBanked : 2;
   __shared__ uint64_t etab[ES == 2 ? 256 : 128 * kExpBanked];
+  // ROT (64QAM, FAST, one symbol per thread, S >= 256: launch_demap): the
+  // points times the channel of the (at most two) codewords of this
+  // workgroup's symbols, formed once per workgroup instead of once per symbol
+  static_assert(!ROT || !EXACT, "ROT: the FAST instance only");
+  __shared__ double crot[ROT ? 4 << MB : 2];
   const long long n = (long long)B * S;
   long long todo = n;
   bool listed = false;
@@ -77,6 +82,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? K
     stage_exp_table(etab);
   else
     stage_exp_table_banked(etab);
+  const int ent0 = (int)((long long)blockIdx.x * blockDim.x / S);
+  if (ROT)
+    for (int t = threadIdx.x; t < (2 << MB); t += blockDim.x) {
+      const int e = ent0 + (t >> MB), k = t & ((1 << MB) - 1);
+      if (e >= B) break;
+      const double2 hh = h[(long long)e * h_stride + (h_sel ? h_sel[e] : 0)];
+      const double cr = cons[2 * k], ci = cons[2 * k + 1];
+      crot[2 * t] = cr * hh.x - ci * hh.y;  // the reference's symbol *= theta_h (demap_symbol_t)
+      crot[2 * t + 1] = cr * hh.y + ci * hh.x;
+    }
   __syncthreads();
   const lds_exptab et = (lds_exptab)etab + (ES == 2 ? 0 : 2 * (threadIdx.x & 15));
   // grid-stride over the symbols: the LDS staging above is paid once per
@@ -88,17 +103,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MB >= 6 ? K
     const int j = (int)(gid - (long long)ent * S);
     const double2 hh = h[(long long)ent * h_stride + (h_sel ? h_sel[ent] : 0)];
     const double2 yy = y[(long long)(ent / reps) * S + j];
-    double out[MB];
-    if constexpr (EXACT) {
+    double out[MB] = {};  // defined for the unconditional stores below
+    bool ok = true;
+    if constexpr (EXACT)
       demap_symbol_t<MB, false>((lds_cons)cl, (lds_exptab)etab, yy.x, yy.y, hh.x, hh.y, var, out);
-    } else if (!demap_symbol_t<MB, true, lds_cons, ES>((lds_cons)cl, et, yy.x, yy.y, hh.x, hh.y, var, out)) {
-      p0[gid * MB] = -1.0;  // the sentinel (a P0 is in [1e-12, 1 - 1e-12])
-      const unsigned k = atomicAdd(d.cnt, 1u);
-      if (k < (unsigned)d.cap) d.idx[k] = (int32_t)gid;
-      continue;
-    }
+    else if (ROT)
+      ok = demap_symbol_t<MB, true, lds_cons, ES, true, ROT>((lds_cons)crot + ((ent - ent0) << (MB + 1)), et, yy.x,
+                                                              yy.y, hh.x, hh.y, var, out);
+    else
+      ok = demap_symbol_t<MB, true, lds_cons, ES>((lds_cons)cl, et, yy.x, yy.y, hh.x, hh.y, var, out);
+    // stored unconditionally: an unproven symbol gets the sentinel p0 = -1 in
+    // its first bit (a P0 is in [1e-12, 1 - 1e-12]) and the EXACT instance
+    // rewrites all its bits; no branch around the stores, so the outputs are
+    // not spilled across a divergent join (64QAM: 48 B per symbol of scratch)
+    if (!EXACT) out[0] = ok ? out[0] : -1.0;
 #pragma unroll
     for (int b = 0; b < MB; ++b) p0[gid * MB + b] = out[b];
+    if (!ok) {
+      const unsigned k = atomicAdd(d.cnt, 1u);
+      if (k < (unsigned)d.cap) d.idx[k] = (int32_t)gid;
+    }
+    if (ROT) break;  // one symbol per thread: no loop state held across the symbol
   }
 }
 
@@ -385,7 +410,17 @@ hipError_t launch_demap(int bits, const double *cons, const double2 *y, int S, i
     KML_DM(2)
     KML_DM(3)
     KML_DM(4)
-    KML_DM(6)
+    case 6:
+      // one symbol per thread and S >= 256: a workgroup's symbols span at most
+      // two codewords, whose rotated points it stages (demap_kernel ROT)
+      if (S >= 256)
+        hipLaunchKernelGGL((demap_kernel<6, false, true>), grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var,
+                           B, p0, d);
+      else
+        hipLaunchKernelGGL((demap_kernel<6, false>), grid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0,
+                           d);
+      hipLaunchKernelGGL((demap_kernel<6, true>), xgrid, blk, 0, s, cons, y, S, reps, h, h_stride, h_sel, var, B, p0, d);
+      break;
 #undef KML_DM
     default:
       return hipErrorInvalidValue;

@@ -99,9 +99,14 @@ __device__ __forceinline__ double exp_core(double x, lds_exptab tab) {
 // (below; the same bits).  The fused QPSK prologue of bp_regular keeps the
 // reference's sequence (LEAN = false): there the lean form measured 0.45 %
 // slower on the headline kernel (profiles/r04_ab15_summary.txt).
-template <int MB, bool FAST, class CP, int ES = 2, bool LEAN = true>
+// ROT (FAST only): cons holds the points already multiplied by the channel,
+// (cr hr - ci hi, cr hi + ci hr) in the reference's operation order
+// (demap_kernel stages them per codeword), and hr, hi are unused: the same
+// values, 6 fewer operations per point.
+template <int MB, bool FAST, class CP, int ES = 2, bool LEAN = true, bool ROT = false>
 __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double yr, double yi, double hr,
                                                double hi, double var, double *out) {
+  static_assert(!ROT || FAST, "pre-rotated points: FAST path only");
   constexpr int KC = 1 << MB;
   // opaque per call: the constellation's LDS loads must not be hoisted out of
   // the caller's symbol loop (64QAM: 128 doubles held live across it)
@@ -115,8 +120,8 @@ __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double 
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
     const double cr = cons[2 * k], ci = cons[2 * k + 1];
-    double sr = cr * hr - ci * hi;  // symbol *= theta_h
-    double si = cr * hi + ci * hr;
+    double sr = ROT ? cr : cr * hr - ci * hi;  // symbol *= theta_h
+    double si = ROT ? ci : cr * hi + ci * hr;
     sr = sr - yr;  // symbol -= yy
     si = si - yi;
     const double n = sr * sr + si * si;
@@ -129,8 +134,13 @@ __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double 
       d = div_rn(n, var);
     }
     pr[k] = -d;
-    if (k == 0 || mx < pr[k]) mx = pr[k];  // *max_element
+    if (!FAST && (k == 0 || mx < pr[k])) mx = pr[k];  // *max_element
   }
+  // FAST: *max_element = -RN(nmin / var): every d_k = RN(n_k / var) once the
+  // proofs pass, and RN(x / var) is non-decreasing in x (var > 0), so the
+  // largest -d_k is -RN(min n_k / var), proven like the others (no
+  // per-point running maximum)
+  if (FAST) mx = -qdiv(nmin, var, rv, dok);
   if (FAST && !(dok && nmin >= 0x1p-512 && nmax <= 0x1p512 && var >= 0x1p-64 && var <= 0x1p64)) return false;
   double sum = 0.0;
   bool eok = true;

@@ -286,7 +286,7 @@ constexpr int kMaxS = 4096;  // 64-symbol words in the lanes of one wave
 #define KML_STAMPS 0
 #endif
 enum { KS_PRO, KS_CLUSTERS, KS_ASSIGN, KS_COMPACT, KS_SUM, KS_ITERS, KS_WORDS, KS_COMPACTIONS, KS_CW, KS_UPDATE, KS_STEPS,
-       KS_SLOTS = 16 };
+       KS_WEAK, KS_SLOTS = 16 };
 __device__ unsigned long long kml_km_stamps[KS_SLOTS];
 #if KML_STAMPS
 // accumulated in thread 0's registers, flushed once per workgroup (KM_FLUSH)
@@ -632,6 +632,28 @@ __device__ __forceinline__ bool screen0(const double2 *cl, double yr, double yi,
 
 __device__ KM_SLOW cplx cdiv_slow(cplx n, cplx dd) { return kml_cdiv(n, dd); }
 
+// A symbol's drift threshold D + g / (2 Cmax), rounded down: the (1 - 2^-20)
+// factor covers the float conversion's rounding in the normal range; below
+// FLT_MIN (where a denormal's relative rounding error is unbounded) it is 0,
+// i.e. the symbol is re-assigned next iteration; past the float range a finite
+// 2^127.
+__device__ __forceinline__ float km_threshold(double drift, double g, double inv2c) {
+  const double td = (drift + g * inv2c) * (1.0 - 0x1p-20);
+  return td < 0x1p-126 ? 0.0f : td < 0x1p127 ? (float)td : 0x1p127f;
+}
+
+// Threshold tiers of the incremental assignment (KML_KM_WEAK): a word's few
+// symbols closest to a decision boundary (the kKmWeak smallest thresholds) are
+// re-assigned on their own, gathered from several words into one pass, while
+// the drift stays below the word's other thresholds; the whole word is
+// re-assigned only when it reaches those.  A CPU model of the rule
+// (PEG2304 / QPSK, 2 dB) re-assigns 2.6 instead of 6.2 whole words per
+// iteration, plus ~10 weak symbols in one gathered pass.
+#ifndef KML_KM_WEAK
+#define KML_KM_WEAK 1
+#endif
+constexpr int kKmWeak = 3;
+
 // kml_cdiv(n, {c, 0}) for a count c >= 1: __divdc3's |c| >= |d| branch with
 // ratio = 0 / c = 0 and denom = 0 * 0 + c = c, where fabs(ratio) > DBL_MIN is
 // false, gives x = (a + 0 * (b / c)) / c and y = (b - 0 * (a / c)) / c, which
@@ -747,7 +769,7 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
   const int Sw = (S + 63) / 64;
 #if KML_STAMPS
   unsigned long long km_prev = __builtin_amdgcn_s_memtime();
-  unsigned long long km_acc[KS_STEPS + 1] = {};
+  unsigned long long km_acc[KS_WEAK + 1] = {};
   KM_COUNT(KS_CW, 1);
 #endif
   const double2 *yy = y + (long long)cw * S;
@@ -838,6 +860,12 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
   // lane w < Sw: word w's membership bits and its threshold min(D(ref) + g / (2 Cmax)); -1: assign
   uint64_t wb = 0;
   float wt = -1.0f;
+#if KML_KM_WEAK
+  // tiers (KML_KM_WEAK): wt is the minimum threshold of the word's kKmWeak weak
+  // symbols (packed 7-bit lane indices in wk, bit 6 = none), wt2 that of the others
+  float wt2 = -1.0f;
+  unsigned wk = 0;
+#endif
   uint64_t wb_list = 0;  // lane w: word w's bits and list offset at the last rebuild
   int excl_list = 0;
   const double *yv = reinterpret_cast<const double *>(yy);
@@ -870,6 +898,95 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
     // assignment (kmeans.cc:36-46) of the words whose decisions the drift may
     // have changed; two words per pass (independent loads, screens and minima)
     int chg = 0;
+#if KML_KM_WEAK
+    {
+      // a full pass over the words whose other symbols' thresholds the drift
+      // reached; a gathered pass over the weak symbols of the words where only
+      // theirs were reached
+      uint64_t need = __ballot(lane < Sw && (!incremental || !(drift < (double)wt2)));
+      uint64_t weakw = incremental ? __ballot(lane < Sw && !(drift < (double)wt) && drift < (double)wt2) : 0ull;
+      // one pass per flagged word, then passes over up to 21 words' weak
+      // symbols (kKmWeak = 3 entries each); the passes share one screen
+      while (need | weakw) {  // wave-uniform
+        const bool full = need != 0;
+        int q = 0, src = 0, b = 0, nw = 0;
+        uint64_t chunk = 0;
+        if (full) {
+          q = __builtin_ctzll(need);
+          need &= need - 1;
+          b = lane;
+        } else {
+          const int rank = __popcll(weakw & ((1ull << lane) - 1));
+          chunk = __ballot(((weakw >> lane) & 1) && rank < 64 / kKmWeak);
+          weakw &= ~chunk;
+          // entry i = kKmWeak n + jj: the jj-th weak symbol of the n-th word of the chunk
+          for (uint64_t c = chunk; c; c &= c - 1, ++nw)  // scalar loop over the chunk's words
+            if (lane / kKmWeak == nw) src = __builtin_ctzll(c);
+          const unsigned pk = (unsigned)__shfl((int)wk, src);
+          b = lane < kKmWeak * nw ? (int)((pk >> (7 * (lane % kKmWeak))) & 0x7F) : 64;
+          q = src;
+        }
+        const int sym = q * 64 + b;
+        const bool valid = b < 64 && sym < S;  // (weak symbols are always valid lanes)
+        const double2 v = yy[valid ? sym : 0];
+        bool m = false;
+        double g = 0.0;
+        const bool dec = screen0<KC>(cl, v.x, v.y, m, g);
+        if (__ballot(valid && !dec))
+          if (valid && !dec) {  // tie band / range: the exact decision
+            m = member0_slow<KC>(cl, v.x, v.y);
+            g = 0.0;
+          }
+        float tt = valid ? km_threshold(drift, g, kc->inv2c) : INFINITY;
+        if (!full) {  // back to the word lanes: the threshold with the decision in its sign bit
+          const float r = m ? -tt : tt;
+          const bool mine = (chunk >> lane) & 1;
+          const int base = kKmWeak * __popcll(chunk & ((1ull << lane) - 1));
+          float nt = INFINITY;
+          uint64_t nb = wb;
+#pragma unroll
+          for (int jj = 0; jj < kKmWeak; ++jj) {
+            const float rj = __shfl(r, base + jj);
+            const int bj = (int)((wk >> (7 * jj)) & 0x7F);
+            if (mine && bj < 64) {
+              nt = fminf(nt, fabsf(rj));
+              nb = (nb & ~(1ull << bj)) | ((uint64_t)(__float_as_uint(rj) >> 31) << bj);
+            }
+          }
+          if (__ballot(mine && nb != wb)) chg = 1;
+          if (mine) {
+            wb = nb;
+            wt = nt;
+          }
+          KM_COUNT(KS_WEAK, 1);
+          continue;
+        }
+        // the kKmWeak smallest thresholds (first lane on ties) are the weak
+        // symbols; the rest's minimum is wt2
+        float t1 = INFINITY;
+        unsigned wkp = 0;
+#pragma unroll
+        for (int jj = 0; jj < kKmWeak; ++jj) {
+          const float mj = wave_min_f(tt);
+          const uint64_t at = __ballot(tt == mj);
+          const int lj = mj < INFINITY ? __builtin_ctzll(at) : 64;  // 64: none
+          if (jj == 0) t1 = mj;
+          wkp |= (unsigned)(lj & 0x7F) << (7 * jj);
+          if (lane == lj) tt = INFINITY;
+        }
+        const float t2 = wave_min_f(tt);
+        const uint64_t bits = __ballot(valid && m);
+        if (it == 0 || bits != lane_u64(wb, q)) chg = 1;
+        if (lane == q) {
+          wb = bits;
+          wt = t1;
+          wt2 = t2;
+          wk = wkp;
+        }
+        KM_COUNT(KS_WORDS, 1);
+      }
+    }
+#else
     {
       uint64_t need = __ballot(lane < Sw && (!incremental || !(drift < (double)wt)));
       while (need) {  // wave-uniform, one flagged word per pass
@@ -901,6 +1018,7 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
         KM_COUNT(KS_WORDS, 1);
       }
     }
+#endif
     KM_STAMP(KS_ASSIGN);
     if (chg) {  // members changed: rebuild the value list (word by word, coalesced loads, lanes = symbols)
       KM_COUNT(KS_COMPACTIONS, 1);
@@ -974,7 +1092,7 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
   }
 #if KML_STAMPS
   if (tid == 0)
-    for (int i = 0; i <= KS_STEPS; ++i) atomicAdd(&kml_km_stamps[i], km_acc[i]);
+    for (int i = 0; i <= KS_WEAK; ++i) atomicAdd(&kml_km_stamps[i], km_acc[i]);
 #endif
   if (lane == 0) {
     if (hat_out) hat_out[cw] = make_double2(hat.re, hat.im);  // the final hatH (clusters_ = c[k] * hatH)

@@ -3,6 +3,7 @@
 // with the properties the kernels rely on.  Prints "plan_errors=0" on success.
 //   plan_check <PEG2304 H> <BG2 H> <PEG8064 H>
 #include <cstdio>
+#include <cstdlib>
 #include <set>
 #include <string>
 #include <vector>
@@ -152,6 +153,22 @@ static void check_partition(const LdpcCode &L) {
       CHECK(P.vaddr[i] >= EG * 16, "cut edge %zu addressed to a row slot", i);
     }
   CHECK(nvx == P.ncut, "vx names %lld cut edges of %d", nvx, P.ncut);
+  // exact balance (member m owns vn[m NG, (m+1) NG) and cn[m MG, (m+1) MG)):
+  // every uncut edge of a column addresses a row slot of its own member whose
+  // row holds that column
+  const int NG = P.NG, dv = L.dv_max, dc = L.dc_max;
+  CHECK(NG * P.G == L.N && P.MG * P.G == L.M, "member sizes %d %d", NG, P.MG);
+  for (int p = 0; p < L.N; p++)
+    for (int k = 0; k < dv; k++) {
+      if (P.vx[(size_t)p * dv + k] >= 0) continue;
+      const int sl = P.vaddr[(size_t)p * dv + k] / 16, r = P.cn[(p / NG) * P.MG + sl / dc];
+      bool has = false;
+      for (int e = L.row_ptr[r]; e < L.row_ptr[r + 1]; e++) has |= L.row_col[e] == P.vn[p];
+      CHECK(has, "column position %d edge %d: row %d of member %d does not hold it", p, k, r, p / NG);
+    }
+  // the refined cut (layout.cpp PartRefiner; the relabelling alone: 6,602)
+  if (!getenv("KML_PART_REFINE") || getenv("KML_PART_REFINE")[0] != '0')
+    CHECK(P.ncut <= (getenv("KML_PART_REFINE_ITERS") ? 6602 : 5700), "cut %d edges", P.ncut);
   for (int x = 0; x < P.ncut; x++) CHECK(seen_x[x] == 1, "mailbox index %d received %d times", x, seen_x[x]);
   printf("partition: %d of %d edges cut, mirror_max %d\n", P.ncut, L.E, P.mirror_max);
 }

@@ -197,7 +197,7 @@ def test_kernel_placement_plans(tmp_path, data_dir):
     within the limits, one degree per paired wave), bp_part's partition."""
     exe = tmp_path / "planc"
     csrc = os.path.join(REPO, "kmldpc_amd", "csrc")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-I", csrc, "-o", str(exe),
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-I", csrc, "-o", str(exe),
                     os.path.join(REPO, "tests", "native", "plan_check.cpp"), os.path.join(csrc, "code.cpp"),
                     os.path.join(csrc, "layout.cpp")], check=True)
     out = subprocess.run([str(exe)] + [os.path.join(data_dir, f) for f in
@@ -215,10 +215,13 @@ def test_host_code_under_sanitizers(tmp_path, data_dir):
     error paths on truncated / garbage H and constellation files and broken
     TOML (tests/native/host_san_check.cpp).  Any sanitizer finding aborts."""
     csrc = os.path.join(REPO, "kmldpc_amd", "csrc")
-    flags = ["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+    flags = ["g++", "-O1", "-g", "-std=c++17", "-pthread", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
              "-fno-omit-frame-pointer", "-I", csrc]
     host = [os.path.join(csrc, f) for f in ("code.cpp", "layout.cpp", "config.cpp", "modem.cpp", "refstream.cpp")]
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    # the partition refinement's annealing at a short schedule (its full length
+    # runs in test_kernel_placement_plans)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1",
+               KML_PART_REFINE_ITERS="3000000")
     hsc, planc = tmp_path / "hsc", tmp_path / "planc"
     builds = [subprocess.Popen(flags + ["-o", str(hsc), os.path.join(REPO, "tests", "native", "host_san_check.cpp")]
                                + host),

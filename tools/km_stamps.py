@@ -53,6 +53,7 @@ def main():
         print(f"  {n:30s} {st[i] / ncw:9.0f} cycles/cw  {st[i] / max(iters, 1):7.0f} /iter  {100 * st[i] / ncw / tot:5.1f}%")
     print(f"  {'total':30s} {tot:9.0f} cycles/cw")
     print(f"  wave-sum steps per iteration (real chain) {st[10] / max(iters, 1):.2f}")
+    print(f"  gathered weak-symbol passes per iteration {st[11] / max(iters, 1):.2f} (KML_KM_WEAK)")
 
 
 if __name__ == "__main__":
