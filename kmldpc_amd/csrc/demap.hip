@@ -209,11 +209,25 @@ __device__ __forceinline__ bool cand_metric_cw(int cw, const DevCode &c, const d
   __syncthreads();
   if (!EXACT && cnt[5]) return false;  // uniform: every thread read the flag after the barrier
   int local[4] = {0, 0, 0, 0};
-  for (int r = tid; r < c.M; r += blockDim.x) {
-    unsigned p = 0;  // byte q: candidate q's parity (bytes of candidates >= nc unused)
-    for (int e = c.row_ptr[r]; e < c.row_ptr[r + 1]; ++e) p ^= *reinterpret_cast<const unsigned *>(hb + 4 * c.row_col[e]);
+  const unsigned *hb32 = reinterpret_cast<const unsigned *>(hb);
+#ifndef KML_CM_ROW6  // (A/B) 0: the generic row loop
+#define KML_CM_ROW6 1
+#endif
+  if (KML_CM_ROW6 && c.regular && c.dc_max == 6) {  // (PEG codes) row r's edges at 6 r: three independent 8-byte loads
+    for (int r = tid; r < c.M; r += blockDim.x) {
+      const int2 *rc = reinterpret_cast<const int2 *>(c.row_col + 6 * r);  // 8-byte aligned (256-aligned base)
+      const int2 e0 = rc[0], e1 = rc[1], e2 = rc[2];
+      const unsigned p = hb32[e0.x] ^ hb32[e0.y] ^ hb32[e1.x] ^ hb32[e1.y] ^ hb32[e2.x] ^ hb32[e2.y];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) local[q] += (p >> (8 * q)) & 1;
+      for (int q = 0; q < 4; ++q) local[q] += (p >> (8 * q)) & 1;
+    }
+  } else {
+    for (int r = tid; r < c.M; r += blockDim.x) {
+      unsigned p = 0;  // byte q: candidate q's parity (bytes of candidates >= nc unused)
+      for (int e = c.row_ptr[r]; e < c.row_ptr[r + 1]; ++e) p ^= hb32[c.row_col[e]];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) local[q] += (p >> (8 * q)) & 1;
+    }
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q)

@@ -103,6 +103,9 @@ __device__ __forceinline__ double exp_core(double x, lds_exptab tab) {
 // (cr hr - ci hi, cr hi + ci hr) in the reference's operation order
 // (demap_kernel stages them per codeword), and hr, hi are unused: the same
 // values, 6 fewer operations per point.
+#ifndef KML_DEMAP_MX_NMIN  // (A/B) 0: the running maximum of the reference's loop
+#define KML_DEMAP_MX_NMIN 1
+#endif
 template <int MB, bool FAST, class CP, int ES = 2, bool LEAN = true, bool ROT = false>
 __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double yr, double yi, double hr,
                                                double hi, double var, double *out) {
@@ -134,13 +137,13 @@ __device__ __forceinline__ bool demap_symbol_t(CP cons, lds_exptab etab, double 
       d = div_rn(n, var);
     }
     pr[k] = -d;
-    if (!FAST && (k == 0 || mx < pr[k])) mx = pr[k];  // *max_element
+    if (!(FAST && KML_DEMAP_MX_NMIN) && (k == 0 || mx < pr[k])) mx = pr[k];  // *max_element
   }
   // FAST: *max_element = -RN(nmin / var): every d_k = RN(n_k / var) once the
   // proofs pass, and RN(x / var) is non-decreasing in x (var > 0), so the
   // largest -d_k is -RN(min n_k / var), proven like the others (no
   // per-point running maximum)
-  if (FAST) mx = -qdiv(nmin, var, rv, dok);
+  if (FAST && KML_DEMAP_MX_NMIN) mx = -qdiv(nmin, var, rv, dok);
   if (FAST && !(dok && nmin >= 0x1p-512 && nmax <= 0x1p512 && var >= 0x1p-64 && var <= 0x1p64)) return false;
   double sum = 0.0;
   bool eok = true;
