@@ -652,7 +652,10 @@ __device__ __forceinline__ float km_threshold(double drift, double g, double inv
 #ifndef KML_KM_WEAK
 #define KML_KM_WEAK 1
 #endif
-constexpr int kKmWeak = 3;
+#ifndef KML_KM_WEAK_K  // weak symbols per word (<= 4: packed 7-bit lane indices)
+#define KML_KM_WEAK_K 3
+#endif
+constexpr int kKmWeak = KML_KM_WEAK_K;
 
 // kml_cdiv(n, {c, 0}) for a count c >= 1: __divdc3's |c| >= |d| branch with
 // ratio = 0 / c = 0 and denom = 0 * 0 + c = c, where fabs(ratio) > DBL_MIN is
@@ -723,6 +726,9 @@ __device__ __forceinline__ cplx cdiv_const(cplx n, cplx dd, const CdivConst &k) 
 #ifndef KML_KM_WAVE_OCC
 #define KML_KM_WAVE_OCC 6  // waves per SIMD (registers <= 512 / OCC): 6 (80 VGPRs, 9 spilled) 2.75 ms, 5 3.04, 4 3.31
 #endif
+#ifndef KML_KM_CAPMUL  // member-list capacity S * CAPMUL / CAPDIV (A/B with the occupancy)
+#define KML_KM_CAPMUL 1
+#endif
 #ifndef KML_KM_CAPDIV
 #define KML_KM_CAPDIV 3
 #endif
@@ -738,7 +744,7 @@ struct KmWaveLds {
   int cap, off_cl, stride;
 };
 __host__ __device__ constexpr KmWaveLds km_wave_lds(int S, int KC) {
-  const int cap = ((S + KML_KM_CAPDIV - 1) / KML_KM_CAPDIV + 7) & ~7;  // (A/B) larger clusters: the fallback sum
+  const int cap = ((S * KML_KM_CAPMUL + KML_KM_CAPDIV - 1) / KML_KM_CAPDIV + 7) & ~7;  // (A/B) larger clusters: the fallback sum
   const int off_cl = 16 * cap;
   // then the cluster points [KC], the constellation [KC] and the launch
   // constants (KmWaveConst): kept in LDS, not in registers across the loop
