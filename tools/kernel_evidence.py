@@ -47,7 +47,8 @@ def parse(name):
     if fam not in CHAIN_FAMILIES or "<" not in n:
         return fam, ""
     targs = [t.strip() for t in n.split("<", 1)[1].split(">")[0].split(",")]
-    exact = targs[-1] == "true"
+    # the EXACT flag: demap_kernel<MB, EXACT, ROT>, the others' last argument
+    exact = (targs[1] if fam == "demap_kernel" and len(targs) > 2 else targs[-1]) == "true"
     if fam == "bp_part_kernel":
         return fam, "exact" if exact else ("fast_tagged" if targs[-2] == "true" else "fast_barrier")
     return fam, "exact" if exact else "fast"
