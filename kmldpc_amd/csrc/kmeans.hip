@@ -723,6 +723,23 @@ __device__ __forceinline__ cplx cdiv_const(cplx n, cplx dd, const CdivConst &k) 
 // per SIMD) and there is no workgroup barrier at all.  The real and the
 // imaginary chains are summed by the same wave one after the other (both in
 // one scan step measured slower: more registers).
+// Member list in per-word segments (KML_KM_SEG): word w's members in
+// ascending order, then -0.0 fillers up to its capacity (members at the last
+// layout + kKmSlack).  x + (-0.0) == x for every x (signed zeros, infinities
+// and NaNs included), so the ordered sum over the list equals the sum over the
+// members, and a word whose members change rewrites its own segment only —
+// the compacted list shifted every later word (a CPU model of the PEG2304 /
+// QPSK trajectories: 6.2 -> 3.4 words reloaded per iteration for 6 % more
+// scanned elements, tools/probe/km_seg_model.py; measured 2.41 -> 2.28 ms per
+// 32,768 blind PEG2304 codewords, slack 2: 2.39 ms — the list passes 320
+// elements, one scan step).
+#ifndef KML_KM_SEG
+#define KML_KM_SEG 1
+#endif
+#ifndef KML_KM_SLACK
+#define KML_KM_SLACK 1
+#endif
+constexpr int kKmSlack = KML_KM_SLACK;
 #ifndef KML_KM_WAVE_OCC
 #define KML_KM_WAVE_OCC 6  // waves per SIMD (registers <= 512 / OCC): 6 (80 VGPRs, 9 spilled) 2.75 ms, 5 3.04, 4 3.31
 #endif
@@ -773,6 +790,10 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
   double2 *cs = cl + KC;                                              // [KC] constellation points
   KmWaveConst *kc = reinterpret_cast<KmWaveConst *>(cl + 2 * KC);
   const int Sw = (S + 63) / 64;
+  // segments pay off where a word holds many members (QPSK / 4PSK: ~16 of 64);
+  // for 16 and 64 points the fillers would lengthen the scanned list by 25 % /
+  // 100 % (64QAM measured 0.48 -> 0.49 ms), so those keep the compacted list
+  constexpr bool kSeg = KML_KM_SEG && KC <= 4;
 #if KML_STAMPS
   unsigned long long km_prev = __builtin_amdgcn_s_memtime();
   unsigned long long km_acc[KS_WEAK + 1] = {};
@@ -873,7 +894,11 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
   unsigned wk = 0;
 #endif
   uint64_t wb_list = 0;  // lane w: word w's bits and list offset at the last rebuild
-  int excl_list = 0;
+  // kSeg: lane w: word w's segment of the value list, offset << 16 | capacity
+  // (members + kKmSlack -0.0 fillers, at most 64); nlist: the list's length
+  int seg = 0, nlist = 0;
+  bool listok = false;
+  int excl_list = 0;  // (!kSeg) lane w: word w's list offset at the last rebuild
   const double *yv = reinterpret_cast<const double *>(yy);
   __builtin_amdgcn_wave_barrier();
   KM_STAMP(KS_PRO);
@@ -1026,7 +1051,45 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
     }
 #endif
     KM_STAMP(KS_ASSIGN);
-    if (chg) {  // members changed: rebuild the value list (word by word, coalesced loads, lanes = symbols)
+    if (kSeg && chg) {  // members changed: rewrite the changed words' segments (coalesced loads, lanes = symbols)
+      KM_COUNT(KS_COMPACTIONS, 1);
+      const int c = __popcll(wb);
+      nmem = __builtin_amdgcn_readlane(wave_inclusive_scan_i(c), 63);
+      // a new layout at the first iteration, after an overflowing list, or when
+      // a word outgrew its segment: every segment sized to its members + slack
+      const bool full = it == 0 || !listok || __ballot(lane < Sw && c > (seg & 0xFFFF)) != 0;
+      if (full) {
+        const int nc = lane < Sw ? min(c + kKmSlack, 64) : 0;
+        const int incl = wave_inclusive_scan_i(nc);
+        seg = ((incl - nc) << 16) | nc;
+        nlist = __builtin_amdgcn_readlane(incl, 63);
+        listok = nlist <= L.cap;
+      }
+      uint64_t need = listok ? __ballot(lane < Sw && (full || wb != wb_list)) : 0ull;
+      wb_list = wb;
+      while (need) {  // wave-uniform, six words' loads in flight
+        int qs[6];
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+          qs[u] = need ? __builtin_ctzll(need) : -1;
+          need &= need - 1;
+        }
+        double2 v[6];
+#pragma unroll
+        for (int u = 0; u < 6; ++u) v[u] = yy[min((qs[u] < 0 ? qs[0] : qs[u]) * 64 + lane, S - 1)];
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+          if (qs[u] >= 0) {
+            const uint64_t bits = lane_u64(wb, qs[u]);
+            const int so = __builtin_amdgcn_readlane(seg, qs[u]), off = so >> 16, cw = so & 0xFFFF;
+            if ((bits >> lane) & 1) vals[off + __popcll(bits & ((1ull << lane) - 1))] = v[u];
+            // the segment's tail: -0.0, the exact identity of the ordered sum
+            if (lane >= __popcll(bits) && lane < cw) vals[off + lane] = make_double2(-0.0, -0.0);
+          }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (!kSeg && chg) {  // members changed: rebuild the value list (word by word, coalesced loads, lanes = symbols)
       KM_COUNT(KS_COMPACTIONS, 1);
       const int c = __popcll(wb);
       const int incl = wave_inclusive_scan_i(c);
@@ -1062,7 +1125,9 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
     KM_STAMP(KS_COMPACT);
     const int n = nmem;
     cnt += n;
-    if (n > L.cap) {  // more members than the list holds (degenerate input): straight from the words
+    const bool fromwords = kSeg ? !listok : n > L.cap;
+    const int nscan = kSeg ? nlist : n;
+    if (fromwords) {  // more members than the list holds (degenerate input): straight from the words
       double acc = lane == 0 ? sr : si;  // lane 0: real chain, lane 1: imaginary chain, ascending j
       for (int w = 0; w < Sw; ++w) {
         const uint64_t bits = lane_u64(wb, w);
@@ -1073,13 +1138,13 @@ __global__ __launch_bounds__(64 * kWaveWpg) __attribute__((amdgpu_waves_per_eu(K
       si = lane_d(acc, 1);
     } else if (scan) {
       int steps = 0;
-      sr = ordered_sum_vals1(sr, vals, 0, n, lane, steps);  // the real chain, then the imaginary one
-      si = ordered_sum_vals1(si, vals, 1, n, lane, steps);
+      sr = ordered_sum_vals1(sr, vals, 0, nscan, lane, steps);  // the real chain, then the imaginary one
+      si = ordered_sum_vals1(si, vals, 1, nscan, lane, steps);
       KM_COUNT(KS_STEPS, steps);
     } else {  // lane 0: real chain, lane 1: imaginary chain
       double acc = lane == 0 ? sr : si;
       if (lane < 2)
-        for (int i = 0; i < n; ++i) acc = acc + reinterpret_cast<const double *>(vals)[2 * i + lane];
+        for (int i = 0; i < nscan; ++i) acc = acc + reinterpret_cast<const double *>(vals)[2 * i + lane];
       sr = lane_d(acc, 0);
       si = lane_d(acc, 1);
     }
