@@ -1068,3 +1068,33 @@ def test_candidate_metric_screen_equals_exact_demap(data_dir, modem, monkeypatch
     assert np.array_equal(r_on["metrics"], r_off["metrics"])
     assert np.array_equal(r_on["chosen"], r_off["chosen"])
     assert np.array_equal(r_on["uu_hat"], r_off["uu_hat"])
+
+
+@pytest.mark.parametrize("matrix,modem,is5g,snr,n", [
+    ("PEG8064regular0.5.txt", "2bits_QPSK.txt", False, 2.2, 120),
+    ("PEG8064regular0.5.txt", "4bit_16QAM_Gray.txt", False, 6.4, 60),
+    ("PEG2304regular0.5.txt", "2bits_4PSK.txt", False, 2.0, 300),
+    ("PEG2304regular0.5.txt", "6bits_64QAM_Gray.txt", False, 10.5, 200),
+    ("5GLDPCBG2a3_R12_K960.txt", "6bits_64QAM_Gray.txt", True, 11.0, 200),
+    ("5GLDPCBG2a3_R12_K960.txt", "2bits_QPSK.txt", True, 2.0, 200),
+])
+def test_cross_product_blind_streams_vs_oracle(data_dir, matrix, modem, is5g, snr, n):
+    """The (code x constellation) pairs beyond the reference fixtures' 40-100
+    codewords: fresh oracle streams (another seed) through the whole blind
+    KmCodec::Decoder path — k-means with the threshold tiers and, for <= 4
+    points, the segmented member list; the candidate metric; the rotated-point
+    64QAM demapper — chosen candidate, h_hat, metrics, BP return value and
+    uu_hat bit-exact against the oracle's receive()."""
+    max_iter = 50 if is5g else 20
+    ctx = ctx_for(data_dir, matrix, modem, is5g, max_iter)
+    oc = oracle_for(data_dir, matrix, is5g, max_iter)
+    om = O.Modem(os.path.join(data_dir, modem))
+    uu, cc, th, y = O.gen_frames(oc, om, snr, n, state=61)
+    r = ctx.decode_frames(y, snr, None)
+    for i in range(n):
+        ref = O.receive(oc, om, y[i], th[i], snr, True)
+        assert r["chosen"][i] == ref["chosen"], i
+        assert np.array_equal(r["h_hat"][i], ref["h_hat"]), i
+        assert np.array_equal(r["metrics"][i], ref["metrics"]), i
+        assert r["ret"][i] == ref["ret"], i
+        assert np.array_equal(r["uu_hat"][i], ref["uu_hat"]), i
