@@ -67,6 +67,23 @@ constexpr int kRedBytes = 16;
 #ifndef KML_VN_AGE_PRIO  // (A/B) 1: VN priorities by wave age for the whole phase (measured +4%: off)
 #define KML_VN_AGE_PRIO 0
 #endif
+// Epilogue latency (stamps: 5.4 K + 1.3 K of ~180 K cycles per codeword): the
+// codeword's reference bits for CntErr go straight from global memory into LDS
+// in its prologue (global_load_lds: no register holds them, the latency hides
+// under the demap / prior check instead of opening the epilogue), and the
+// workgroup sums its counters in LDS, flushed with one global atomic each when
+// the workgroup leaves.
+#ifndef KML_REG_EPI_LDS
+#define KML_REG_EPI_LDS 1
+#endif
+// The next queue entry is taken at the start of a codeword's epilogue (thread
+// 0's atomic in flight under CntErr and the epilogue's barrier) instead of
+// between two barriers at the top of the loop: one barrier and the atomic's
+// round trip leave the per-codeword critical path.
+#ifndef KML_REG_QUEUE_EARLY
+#define KML_REG_QUEUE_EARLY 1
+#endif
+constexpr int kRegMaxKw = 64;  // K <= N <= 2304 (bp_regular_threads): 36 words
 #if KML_STAMPS
 __device__ unsigned long long kml_reg_stamps[8];
 // per wave (lane 0), summed over codewords: [0] VN compute, [1] VN barrier
@@ -433,6 +450,8 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
   // fused demap: the constellation and the exp table in LDS (demap_common.hpp)
   __shared__ double dcons[DMB > 0 ? (2 << DMB) : 2];
   __shared__ uint64_t detab[DMB > 0 ? 256 : 1];
+  __shared__ uint64_t refw[kRegMaxKw];                  // KML_REG_EPI_LDS: this codeword's reference bits
+  __shared__ unsigned long long wcnt[CNT_CONVERGED + 1];  // KML_REG_EPI_LDS: the workgroup's counters
   double *p0s = reinterpret_cast<double *>(smem + p0s_offset(c.E, c.N));
   if constexpr (DMB > 0) {
     for (int k = threadIdx.x; k < (2 << DMB); k += T) dcons[k] = a.sym_cons[k];
@@ -479,18 +498,33 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
   unsigned long long rs_prev = __builtin_amdgcn_s_memtime(), rs_acc[8] = {};
 #endif
   const int B = a.B_dev ? (int)*a.B_dev : a.B;  // the exact kernel: the FAST kernel's defer count
+  const bool cnt_lds = KML_REG_EPI_LDS && a.counters;
+  const bool ref_pre = KML_REG_EPI_LDS && a.ref_bits && a.iter_count > 0;  // (c.Kw <= kRegMaxKw: host check)
+  if (cnt_lds && tid <= CNT_CONVERGED) wcnt[tid] = 0;  // ordered by the loop's first barrier
+  if (KML_REG_QUEUE_EARLY && tid == 0) {  // the first entry; then each codeword's epilogue takes the next
+    red[3] = (int)atomicAdd(queue, 1u);
+    red[0] = 0;
+    red[1] = 0;
+  }
   for (;;) {
     __syncthreads();
-    if (tid == 0) {
-      red[3] = (int)atomicAdd(queue, 1u);
-      red[0] = 0;
-      red[1] = 0;
+    if (!KML_REG_QUEUE_EARLY) {
+      if (tid == 0) {
+        red[3] = (int)atomicAdd(queue, 1u);
+        red[0] = 0;
+        red[1] = 0;
+      }
+      __syncthreads();
     }
-    __syncthreads();
     const int entry = red[3];
     REG_STAMP(0);
     if (entry >= B) break;
     const int cw = a.cw_idx ? a.cw_idx[entry] : entry;
+    if (ref_pre && tid < 2 * c.Kw)  // one dword per lane (the first waves), in flight through the prologue
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const unsigned *>(a.ref_bits + (long long)cw * c.Kw) + tid,
+                                       (__attribute__((address_space(3))) void *)(reinterpret_cast<unsigned *>(refw) +
+                                                                                  (tid & ~63)),
+                                       4, 0, 0);
     const double *p0;
     bool dok = true;  // FAST kernel: every symbol's FAST demap proven (else the exact kernel demaps the codeword)
     if constexpr (DMB > 0) {  // ModemLinearSystem::DeMapping of this codeword into LDS
@@ -524,6 +558,8 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
       pv[r] = (vcol[r] >= c.punct) ? p0[vcol[r] - c.punct] : 0.5;
       ok = ok && fast_prior_ok(pv[r], plo);
     }
+    // the LDS writes land before wave 0 passes the next barrier (the barriers wait lgkmcnt only)
+    if (ref_pre) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const bool fast = wg_all<T / 64>(ok ? 1 : 0, pflags) && (fast_allowed & 1);
     REG_STAMP(2);
 
@@ -537,7 +573,10 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
         if (tid == 0 && a.counters) atomicAdd(&a.counters[CNT_REDONE], 1ull);
       }
       if (defer) {
-        if (tid == 0) a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = cw;
+        if (tid == 0) {
+          a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = cw;
+          if (KML_REG_QUEUE_EARLY) red[3] = (int)atomicAdd(queue, 1u);  // (every thread has read red[3])
+        }
         continue;
       }
     } else {
@@ -546,6 +585,8 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
     }
 
     REG_STAMP(3);
+    unsigned nxt = 0;  // KML_REG_QUEUE_EARLY: the next entry, in flight through the epilogue
+    if (KML_REG_QUEUE_EARLY && tid == 0) nxt = atomicAdd(queue, 1u);
 #if KML_STAMPS
     if (tid == 0) {
       rs_acc[6] += 1;
@@ -577,12 +618,13 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
         if (cnt) atomicAdd(&red[0], cnt);
       }
       if (a.ref_bits) {  // CntErr (sourcesink.cc:29-47): two 64-bit words per wave and round, loads first
-        const uint64_t *ref = a.ref_bits + (long long)cw * c.Kw;
+        const uint64_t *ref = a.ref_bits + (long long)cw * c.Kw;  // (KML_REG_EPI_LDS = 0)
         const int lane = tid & 63;
         int errs = 0;
         for (int w0 = tid >> 6; w0 < c.Kw; w0 += 2 * (T / 64)) {
           const int w1 = w0 + T / 64;
-          const uint64_t r0 = ref[w0], r1 = w1 < c.Kw ? ref[w1] : 0ull;
+          const uint64_t r0 = KML_REG_EPI_LDS ? refw[w0] : ref[w0];
+          const uint64_t r1 = w1 < c.Kw ? (KML_REG_EPI_LDS ? refw[w1] : ref[w1]) : 0ull;
           const int i0 = w0 * 64 + lane, i1 = w1 * 64 + lane;
           const int b0 = i0 < c.K ? cch[ipos[i0]] : 0;
           const int b1 = i1 < c.K && w1 < c.Kw ? cch[ipos[i1]] : 0;
@@ -600,21 +642,30 @@ __global__ __launch_bounds__(T) void bp_regular_kernel(DevCode c, BpLaunch a, un
       if (a.cw_err && a.ref_bits) a.cw_err[cw] = a.iter_count > 0 ? red[1] : 0;
       if (a.iters) a.iters[cw] = iter;
       if (a.counters) {
+        unsigned long long *ct = cnt_lds ? wcnt : a.counters;  // (LDS: flushed at the exit)
         const unsigned long long vn = conv ? (unsigned long long)iter + 1 : (unsigned long long)iter;
-        atomicAdd(&a.counters[CNT_VN_PHASES], vn);
-        atomicAdd(&a.counters[CNT_CN_PHASES], (unsigned long long)iter);
-        if (conv) atomicAdd(&a.counters[CNT_CONVERGED], 1ull);
+        atomicAdd(&ct[CNT_VN_PHASES], vn);
+        atomicAdd(&ct[CNT_CN_PHASES], (unsigned long long)iter);
+        if (conv) atomicAdd(&ct[CNT_CONVERGED], 1ull);
         if (a.ref_bits && a.iter_count > 0) {
           const int errs = red[1];
-          atomicAdd(&a.counters[CNT_ERR_BIT], (unsigned long long)errs);
-          atomicAdd(&a.counters[CNT_ERR_BLK], errs > 0 ? 1ull : 0ull);
-          atomicAdd(&a.counters[CNT_TOT_BIT], (unsigned long long)c.K);
-          atomicAdd(&a.counters[CNT_TOT_BLK], 1ull);
+          atomicAdd(&ct[CNT_ERR_BIT], (unsigned long long)errs);
+          atomicAdd(&ct[CNT_ERR_BLK], errs > 0 ? 1ull : 0ull);
+          atomicAdd(&ct[CNT_TOT_BIT], (unsigned long long)c.K);
+          atomicAdd(&ct[CNT_TOT_BLK], 1ull);
         }
+      }
+      if (KML_REG_QUEUE_EARLY) {  // after the reads above; read by all after the loop's barrier
+        red[3] = (int)nxt;
+        red[0] = 0;
+        red[1] = 0;
       }
     }
     REG_STAMP(5);
   }
+  if (cnt_lds && tid == 0)  // the workgroup's sums (only thread 0 wrote them)
+    for (int i = 0; i <= CNT_CONVERGED; ++i)
+      if (wcnt[i]) atomicAdd(&a.counters[i], wcnt[i]);
 #if KML_STAMPS
   if (tid == 0)
     for (int i = 0; i < 8; ++i) atomicAdd(&kml_reg_stamps[i], rs_acc[i]);
@@ -644,7 +695,7 @@ hipError_t launch_reg_one(const DevCode &c, const BpLaunch &a, hipStream_t s, in
 template <int T, int RV, int RC, int DV, int DC, bool SYN, int DMB>
 hipError_t launch_reg_t(const DevCode &c, const BpLaunch &a, hipStream_t s, int fast_allowed) {
   const size_t lds = reg_lds_bytes(c.E, c.N, c.K, DMB);
-  if (lds > 160 * 1024 || c.K > 65536 || c.N > 65536) return hipErrorNotSupported;
+  if (lds > 160 * 1024 || c.K > 65536 || c.N > 65536 || c.Kw > kRegMaxKw) return hipErrorNotSupported;
   if (!(fast_allowed & 1)) return launch_reg_one<T, RV, RC, DV, DC, SYN, DMB, true>(c, a, s, 0);
   if (!a.defer_idx || !a.defer_cnt) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(a.defer_cnt, 0, sizeof(unsigned), s);
