@@ -520,6 +520,9 @@ __device__ __forceinline__ int part_iterations(const BpLaunch &a, int M, int N, 
 #ifndef KML_PART_VN_AGE_PRIO
 #define KML_PART_VN_AGE_PRIO 0
 #endif
+#ifndef KML_PART_QUEUE_EARLY  // the next entry taken under the outputs (bp_part_kernel's loop)
+#define KML_PART_QUEUE_EARLY 1
+#endif
 constexpr unsigned kTagHi = 0x80000000u;  // bit 63 of a message word (hi dword bit 31)
 constexpr unsigned kHdHi = 0x40000000u;   // bit 62: hard decision (v2c first word)
 
@@ -1029,14 +1032,25 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
   // from the device (a.B_dev).
   const int B = a.B_dev ? (int)*a.B_dev : a.B;  // (read again: every read sees the finished count)
 
+  // KML_PART_QUEUE_EARLY: after a decoded codeword, member 0 has taken the
+  // next entry during the outputs and published it before their closing
+  // barrier, and clears the sums after reading them, so the next codeword
+  // starts without a group barrier; after a deferred codeword (no outputs, a
+  // group-uniform branch) and at the start, the entry is taken here.
+  bool top_sync = true;
   for (;;) {
-    if (member == 0 && tid == 0) {
-      __hip_atomic_store(&gs->cw, atomicAdd(queue, 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&gs->errs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&gs->pcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (top_sync) {
+      if (member == 0 && tid == 0) {
+        __hip_atomic_store(&gs->cw, atomicAdd(queue, 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&gs->errs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&gs->pcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (tid == 0) spcnt = 0;
+      if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;
+    } else if (tid == 0) {
+      spcnt = 0;  // (read by this thread before the outputs' closing barrier)
     }
-    if (tid == 0) spcnt = 0;
-    if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;
+    top_sync = !KML_PART_QUEUE_EARLY;
     const int entry = (int)ld_rlx(&gs->cw);
     if (entry >= B) break;
     // a deferred entry with bit 31 set: a codeword the tagged launch stopped on
@@ -1074,6 +1088,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
     if constexpr (TAGGED) {
       if (!fast || !same_xcd) {  // to the barrier-exchange launches (bit 31: the exact one)
         if (member == 0 && tid == 0) a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = fast ? cw : (int)((unsigned)cw | 0x80000000u);
+        top_sync = true;
         continue;
       }
       const int st = part_iterations_tagged<kG, T, RV, RC, RX, SYN>(a, c.M, cw, gs, g, &sfail, &sdead, member, abort,
@@ -1086,6 +1101,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
           a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = (int)((unsigned)cw | 0x80000000u);
           if (a.counters) atomicAdd(&a.counters[CNT_REDONE], 1ull);
         }
+        top_sync = true;
         continue;
       }
     } else if constexpr (!EXACT) {
@@ -1100,6 +1116,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
           a.defer_idx[atomicAdd(a.defer_cnt, 1u)] = cw;
           if (fast && a.counters) atomicAdd(&a.counters[CNT_REDONE], 1ull);
         }
+        top_sync = true;
         continue;
       }
     } else {
@@ -1110,6 +1127,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
     }
 
     // ---- outputs
+    unsigned nxt = 0;  // KML_PART_QUEUE_EARLY: the next entry, in flight through the outputs
+    if (KML_PART_QUEUE_EARLY && member == 0 && tid == 0) nxt = atomicAdd(queue, 1u);
     if (a.iter_count > 0) {
       if constexpr (tagged) {
         // a member holds the decisions of its own columns (double-buffered by
@@ -1173,10 +1192,17 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1))) void bp_
         }
       }
     }
+    // (every member read gs->cw at this codeword's start, several barriers ago)
+    if (KML_PART_QUEUE_EARLY && member == 0 && tid == 0)
+      __hip_atomic_store(&gs->cw, nxt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (part_barrier<kG>(gs, bst, nb, same_xcd, abort, nullptr) < 0) return;  // the members' sums are complete
     if (member == 0 && tid == 0) {
       const int errs = (int)ld_rlx(&gs->errs);
       const int pc = (int)ld_rlx(&gs->pcnt);
+      if (KML_PART_QUEUE_EARLY) {  // no member adds to the sums before the next codeword's flag barrier
+        __hip_atomic_store(&gs->errs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&gs->pcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       if (a.ret) a.ret[cw] = iter + (iter < a.max_iter);
       if (a.iters) a.iters[cw] = iter;
       if (a.parity_cnt) a.parity_cnt[cw] = a.iter_count > 0 ? pc : 0;
